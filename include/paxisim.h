@@ -1,0 +1,235 @@
+/*
+ * paxisim.h — C-ABI of the MI355X batched Paxi simulator (drop-in boundary).
+ *
+ * What this boundary replaces in the reference (acharapko/paxi, Go):
+ *   - `server -sim` (server/server.go:87-101): one goroutine per replica over
+ *     the `chan` transport (transport.go:238-278) and the reflection
+ *     dispatcher (node.go:79-115).  Here: millions of independent clusters,
+ *     one lane per (cluster, replica), device mailboxes instead of channels.
+ *   - paxi.Config (config.go:14-35, Load 97-114: n, z, npz)   -> paxisim_config
+ *   - Socket fault injection Drop/Slow/Flaky/Crash (socket.go:163-199) and the
+ *     filter order crash->drop->flaky->slow in Send (socket.go:66-109)
+ *                                                             -> paxisim_fault
+ *   - Benchmark closed-loop workers (benchmark.go:246-275)   -> paxisim_workload
+ *   - paxos.NewPaxos options Q1/Q2/ReplyWhenCommit (paxos/paxos.go:35-58),
+ *     Quorum predicates (quorum.go:55-119)                   -> q1/q2/fz fields
+ *   - HTTPClient.Consensus agreement check (client.go:279-320) -> paxisim_check
+ *
+ * Conventions: every call returns 0 or a negative PAXISIM_E* code and never
+ * aborts; the message of the last failure on the calling thread is returned
+ * by paxisim_last_error().  The library owns all device memory; the caller
+ * owns the host buffers it passes in.  Calls on one handle must be
+ * serialized (mirrors the reference's one-handler-goroutine-per-replica);
+ * distinct handles (one per GPU) may be driven from parallel host threads.
+ *
+ * The simulation semantics (delivery schedule, bounded-window rules, PRNG)
+ * are specified in DESIGN.md §3; the CPU oracle under oracle/ restates them
+ * from the reference's Go handlers and is the parity checker.
+ */
+#ifndef PAXISIM_H
+#define PAXISIM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PAXISIM_ABI_VERSION 1
+
+#define PAXISIM_MAX_N        16  /* replicas per cluster (ack masks are u16) */
+#define PAXISIM_MAX_ZONES    16
+#define PAXISIM_MAX_WORKERS  32  /* closed-loop client workers per cluster */
+#define PAXISIM_MAX_FAULTS   64  /* scripted fault windows per handle */
+#define PAXISIM_MAX_WINDOW   64  /* log window slots per replica */
+#define PAXISIM_MAX_MBOX     64  /* records per (link, arrival-step) bucket */
+#define PAXISIM_MAX_DELAY    14  /* Slow delay, in steps */
+#define PAXISIM_CLIENT_SRC   31  /* request origin: the client (HTTP path, http.go:99) */
+
+/* ---- error codes ---- */
+#define PAXISIM_OK          0
+#define PAXISIM_EINVAL     -1   /* bad argument / config */
+#define PAXISIM_ENOMEM     -2   /* device or host allocation failed */
+#define PAXISIM_EDEVICE    -3   /* HIP runtime error */
+#define PAXISIM_EUNSUPP    -4   /* feature not built */
+#define PAXISIM_ERANGE     -5   /* cluster range outside the handle */
+
+/* ---- protocols (server/server.go:38-84 algorithm switch) ---- */
+enum paxisim_protocol {
+  PAXISIM_PAXOS  = 0,   /* paxos/paxos.go + paxos/replica.go */
+  PAXISIM_ABD    = 1,   /* abd/replica.go */
+  PAXISIM_WPAXOS = 2    /* wpaxos/replica.go + wpaxos/kpaxos.go */
+};
+
+/* ---- quorum predicates (quorum.go) ---- */
+enum paxisim_quorum {
+  PAXISIM_Q_MAJORITY     = 0,  /* size > n/2              quorum.go:60-62  */
+  PAXISIM_Q_ALL          = 1,  /* size == n               quorum.go:55-57  */
+  PAXISIM_Q_FAST         = 2,  /* size >= n*3/4           quorum.go:65-67  */
+  PAXISIM_Q_GRID_ROW     = 3,  /* AllZones                quorum.go:70-72,85-87 */
+  PAXISIM_Q_ZONE_MAJORITY= 4,  /*                         quorum.go:75-82  */
+  PAXISIM_Q_GRID_COLUMN  = 5,  /*                         quorum.go:90-97  */
+  PAXISIM_Q_FGRID_Q1     = 6,  /* zones w/ majority >= z-fz  quorum.go:100-108 */
+  PAXISIM_Q_FGRID_Q2     = 7   /* zones w/ majority >= fz+1  quorum.go:111-119 */
+};
+
+/* ---- message types (one 16-byte record each) ---- */
+enum paxisim_msg {
+  PAXISIM_MSG_NONE      = 0,
+  PAXISIM_MSG_REQUEST   = 1,  /* paxi.Request (message.go:24-30), forwarded via socket */
+  PAXISIM_MSG_REPLY     = 2,  /* paxi.Reply (message.go:42-48) back to the forwarder */
+  PAXISIM_MSG_P1A       = 3,  /* paxos/msg.go:19-21 */
+  PAXISIM_MSG_P1B       = 4,  /* paxos/msg.go:33-37 (header; payload follows) */
+  PAXISIM_MSG_P1B_ENTRY = 5,  /* one CommandBallot of P1b.Log */
+  PAXISIM_MSG_P2A       = 6,  /* paxos/msg.go:44-48 */
+  PAXISIM_MSG_P2B       = 7,  /* paxos/msg.go:55-59 */
+  PAXISIM_MSG_P3        = 8,  /* paxos/msg.go:66-70 */
+  PAXISIM_MSG_GET       = 9,  /* abd/msg.go:17-21 */
+  PAXISIM_MSG_GETREPLY  = 10, /* abd/msg.go:24-30 */
+  PAXISIM_MSG_SET       = 11, /* abd/msg.go:33-39 */
+  PAXISIM_MSG_SETREPLY  = 12, /* abd/msg.go:42-46 */
+  PAXISIM_MSG_LEADERCHG = 13, /* wpaxos/msg.go:78-84 */
+  PAXISIM_NMSG          = 16
+};
+
+/* ---- per-replica / per-cluster flags ---- */
+#define PAXISIM_F_WOVF      0x01u  /* an entry beyond execute+W was not stored */
+#define PAXISIM_F_GHOST     0x02u  /* an entry below execute was not (re)created */
+#define PAXISIM_F_MBOX_OVF  0x04u  /* a send found its mailbox bucket full: message lost */
+#define PAXISIM_F_PEND_OVF  0x08u  /* pending-request / forwards table full */
+#define PAXISIM_F_UNFAITHFUL 0x10u /* bounded model may differ from unbounded Go from here */
+#define PAXISIM_F_POISON    0x20u  /* the Go reference would panic here; cluster frozen */
+#define PAXISIM_F_BALLOT_OVF 0x40u /* ballot counter beyond 2^27 */
+
+/* ---- scripted faults (socket.go:163-199; http.go:137-162 admin hooks) ---- */
+enum paxisim_fault_kind {
+  PAXISIM_FAULT_DROP  = 0,  /* Drop(to, t): src->dst sends dropped            */
+  PAXISIM_FAULT_SLOW  = 1,  /* Slow(to, d, t): src->dst delayed param steps   */
+  PAXISIM_FAULT_FLAKY = 2,  /* Flaky(to, p, t): dropped w.p. param ppm        */
+  PAXISIM_FAULT_CRASH = 3   /* Crash(t): replica src; step_to=UINT32_MAX = forever (G11) */
+};
+#define PAXISIM_ALL_DST 0xFFu
+
+typedef struct paxisim_config {
+  uint32_t protocol;          /* enum paxisim_protocol */
+  uint32_t n_zones;           /* Z (config.go:113) */
+  uint32_t npz[PAXISIM_MAX_ZONES]; /* nodes per zone; replica ids are "z.n", z,n >= 1,
+                                      indexed in IDs.Less order (id.go:61-69) */
+  uint32_t q1, q2;            /* enum paxisim_quorum for phase 1 / phase 2 */
+  uint32_t fz;                /* FGrid f_z (wpaxos/replica.go:11) */
+  uint32_t thrifty;           /* config.Thrifty (paxos.go:126) */
+  uint32_t ephemeral_leader;  /* -ephemeral_leader (paxos/replica.go:12) */
+  uint32_t reply_when_commit; /* Paxos.ReplyWhenCommit (paxos.go:37) */
+  uint32_t adaptive;          /* WPaxos -adaptive (wpaxos/replica.go:10) */
+  uint32_t policy_threshold;  /* consecutive policy n (policy.go:55-69) */
+  uint32_t window;            /* W: log window per replica (power of 2, 8..64) */
+  uint32_t mbox_cap;          /* M: records per (link, arrival-step) bucket */
+  uint32_t max_delay;         /* largest Slow delay in steps (<= PAXISIM_MAX_DELAY) */
+  uint32_t keys;              /* keys per cluster (ABD/WPaxos instances) */
+  uint32_t steps_per_launch;  /* HIP backend: steps fused per kernel launch (0 = auto) */
+  int32_t  device;            /* HIP device ordinal */
+  uint64_t clusters;          /* clusters held by this handle */
+  uint64_t cluster_base;      /* global id of local cluster 0 (multi-GPU sharding) */
+  uint64_t seed;
+} paxisim_config;
+
+typedef struct paxisim_workload {
+  uint32_t outstanding;       /* closed-loop workers per cluster (Bconfig.Concurrency) */
+  uint32_t max_requests;      /* per worker; 0 = unlimited (Bconfig.N) */
+  uint32_t write_ppm;         /* P(write) in parts per million (Bconfig.W) */
+  uint32_t locality_ppm;      /* WPaxos: P(key from the worker's own zone) */
+  uint32_t target[PAXISIM_MAX_WORKERS]; /* replica each worker sends to */
+} paxisim_workload;
+
+/* Random fault process, applied per (cluster, src, dst) link every step. */
+typedef struct paxisim_fault_process {
+  uint32_t drop_ppm;          /* P(a drop window starts) per step per idle link */
+  uint32_t drop_len;          /* window length in steps */
+  uint32_t slow_ppm;          /* P(a slow window starts) per step per idle link */
+  uint32_t slow_len;
+  uint32_t slow_min, slow_max;/* delay drawn uniformly from [min,max] steps */
+} paxisim_fault_process;
+
+typedef struct paxisim_fault {
+  uint32_t kind;              /* enum paxisim_fault_kind */
+  uint32_t src, dst;          /* replica indices; dst may be PAXISIM_ALL_DST */
+  uint32_t param;             /* SLOW: delay steps; FLAKY: ppm */
+  uint64_t cluster_lo, cluster_hi; /* GLOBAL cluster ids, [lo, hi) */
+  uint32_t step_from, step_to;     /* active for step_from <= t < step_to */
+} paxisim_fault;
+
+/* Per-replica snapshot (read_state). */
+typedef struct paxisim_replica_state {
+  uint64_t ballot;            /* 64-bit Ballot (ballot.go:15-17) */
+  int32_t  slot;              /* highest slot (paxos.go:30) */
+  int32_t  execute;           /* next slot to execute (paxos.go:27) */
+  uint32_t active;
+  uint32_t flags;             /* PAXISIM_F_* raised by this replica */
+  uint64_t digest;            /* hash chain of executed (slot, command) */
+  uint32_t p1_acks;           /* phase-1 ack mask */
+  uint32_t npending;          /* len(p.requests) */
+  uint32_t delivered[PAXISIM_NMSG]; /* socket messages consumed by handlers, by type */
+  uint32_t client_requests;   /* client requests handled (HTTP path) */
+  uint32_t sent;              /* Send() calls (incl. dropped) */
+  uint32_t dropped;           /* sends removed by crash/drop/flaky, or lost to unknown id */
+  uint32_t discarded;         /* inbound messages discarded while crashed (socket.go:111-118) */
+  uint32_t commits;           /* leader commit events (paxos.go:291-292) / ABD Done */
+  uint32_t replies;           /* replies delivered to the client */
+  uint32_t executed_writes;   /* reserved */
+  uint32_t pad;
+} paxisim_replica_state;
+
+/* Whole-handle totals (sum over clusters and replicas). */
+typedef struct paxisim_stats {
+  uint64_t steps;             /* steps simulated so far */
+  uint64_t clusters;
+  uint64_t delivered[PAXISIM_NMSG];
+  uint64_t delivered_total;   /* socket messages delivered (the metric) */
+  uint64_t client_requests;
+  uint64_t sent, dropped, discarded;
+  uint64_t commits;           /* committed slots (the second metric) */
+  uint64_t replies;
+  uint64_t flagged[8];        /* clusters with flag bit i set */
+} paxisim_stats;
+
+typedef struct paxisim paxisim;   /* opaque handle */
+
+int  paxisim_abi_version(void);
+const char* paxisim_last_error(void);
+
+/* Create a handle.  All clusters start at step 0 with empty state; worker w's
+ * first request is waiting at its target replica at step 0. */
+int  paxisim_create(const paxisim_config* cfg, const paxisim_workload* wl,
+                    const paxisim_fault_process* fp, paxisim** out);
+int  paxisim_destroy(paxisim* h);
+
+/* Add a scripted fault window (Drop/Slow/Flaky/Crash). */
+int  paxisim_fault_add(paxisim* h, const paxisim_fault* f);
+
+/* Advance every cluster of the handle by nsteps virtual steps. */
+int  paxisim_step(paxisim* h, uint32_t nsteps);
+int  paxisim_sync(paxisim* h);
+
+/* Totals over the handle. */
+int  paxisim_stats_get(paxisim* h, paxisim_stats* out);
+
+/* Per-replica snapshot of local clusters [cluster_lo, cluster_lo+n): out has
+ * n*N records, cluster-major. */
+int  paxisim_read_state(paxisim* h, uint64_t cluster_lo, uint64_t n,
+                        paxisim_replica_state* out);
+
+/* Agreement scan (client.go:279-320 / tla Safety): number of clusters in
+ * which two replicas executed different commands in the same slot. */
+int  paxisim_check(paxisim* h, uint64_t* violations);
+
+/* Device time of the step kernels since the last reset (HIP events on the
+ * launch stream), and the number of launches. */
+int  paxisim_kernel_time(paxisim* h, double* ms, uint64_t* launches, int reset);
+
+/* Bytes of device memory held by the handle. */
+int  paxisim_device_bytes(paxisim* h, uint64_t* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PAXISIM_H */

@@ -1,0 +1,1085 @@
+/*
+ * oracle.c — single-threaded CPU restatement of Paxi's simulation-mode hot
+ * path under the delivery schedule of DESIGN.md §3.
+ *
+ * TEST INFRASTRUCTURE ONLY (see oracle.h): the parity checker for the HIP
+ * product path and the source of the CPU baseline timing.  It is written to
+ * read like the Go it restates — one function per reference handler, each
+ * citing the file:line it follows — not to be fast.
+ *
+ * Parity pinning: see oracle.h and DESIGN.md §4 (Go toolchain absent; pinned
+ * by ballot_test.go / checker_test.go KATs and hand-derived KATs).
+ */
+#include "oracle.h"
+
+#include <pthread.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+static __thread char g_err[256];
+static int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+  return code;
+}
+const char* oracle_last_error(void) { return g_err; }
+
+/* ------------------------------------------------------------------------ */
+/* PRNG: counter-based, keyed by (seed, cluster, step, tag). */
+/* ------------------------------------------------------------------------ */
+static inline uint64_t mix64(uint64_t z) {
+  z ^= z >> 30; z *= 0xbf58476d1ce4e5b9ULL;
+  z ^= z >> 27; z *= 0x94d049bb133111ebULL;
+  z ^= z >> 31;
+  return z;
+}
+static inline uint64_t cluster_key(uint64_t seed, uint64_t gid) {
+  return mix64(seed ^ mix64(gid + 0x9E3779B97F4A7C15ULL));
+}
+static inline uint64_t draw(uint64_t kc, uint32_t t, uint32_t tag) {
+  return mix64(kc ^ mix64(((uint64_t)t << 32) | tag));
+}
+#define TAG(p, a, b) (((uint32_t)(p) << 28) | ((uint32_t)(a) << 20) | (uint32_t)(b))
+enum { PUR_ORDER = 1, PUR_LINK = 2, PUR_SLOWD = 3, PUR_FLAKY = 4, PUR_WL = 5 };
+static inline int ppm_hit(uint32_t x, uint32_t ppm) {
+  return (uint32_t)(((uint64_t)x * 1000000ULL) >> 32) < ppm;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Ballot / ID (ballot.go:15-52, id.go:14-69).  In-simulation a ballot is      */
+/* kept compressed as (n << 4) | r, r = replica index in IDs.Less order, which */
+/* preserves the uint64 order of (n<<32 | zone<<16 | node).                    */
+/* ------------------------------------------------------------------------ */
+#define NO_ID 0xFFu
+static inline uint32_t bal_id(uint32_t b) { return b ? (b & 15u) : NO_ID; } /* Ballot.ID() ballot.go:43-47; 0 -> "0.0" */
+static inline uint32_t bal_next(uint32_t b, uint32_t self) {                /* Ballot.Next ballot.go:50-52 */
+  return (((b >> 4) + 1u) << 4) | self;
+}
+
+uint64_t oracle_new_ballot(uint32_t n, uint32_t zone, uint32_t node) { /* NewBallot ballot.go:15-17 */
+  return ((uint64_t)n << 32) | ((uint64_t)zone << 16) | (uint64_t)node;
+}
+uint64_t oracle_ballot_next(uint64_t b, uint32_t zone, uint32_t node) {
+  return oracle_new_ballot((uint32_t)(b >> 32) + 1u, zone, node);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Quorum predicates (quorum.go:55-119) over an ack mask.                      */
+/* ------------------------------------------------------------------------ */
+static int popc(uint32_t x) { return __builtin_popcount(x); }
+
+static int quorum_eval(uint32_t kind, uint32_t fz, uint32_t nz, const uint32_t* npz,
+                       const uint32_t* zmask, uint32_t n, uint32_t mask) {
+  int size = popc(mask);
+  uint32_t z, zones_any = 0, zones_maj = 0, col = 0, zmaj = 0;
+  for (z = 0; z < nz; z++) {
+    uint32_t c = (uint32_t)popc(mask & zmask[z]);
+    if (c > 0) zones_any++;
+    if (c > npz[z] / 2) { zones_maj++; zmaj = 1; }
+    if (c == npz[z]) col = 1;
+  }
+  switch (kind) {
+    case PAXISIM_Q_MAJORITY:      return size > (int)(n / 2);           /* quorum.go:60-62 */
+    case PAXISIM_Q_ALL:           return size == (int)n;                /* quorum.go:55-57 */
+    case PAXISIM_Q_FAST:          return size >= (int)(n * 3 / 4);      /* quorum.go:65-67 */
+    case PAXISIM_Q_GRID_ROW:      return zones_any == nz;               /* quorum.go:70-72,85-87 */
+    case PAXISIM_Q_ZONE_MAJORITY: return (int)zmaj;                     /* quorum.go:75-82 */
+    case PAXISIM_Q_GRID_COLUMN:   return (int)col;                      /* quorum.go:90-97 */
+    case PAXISIM_Q_FGRID_Q1:      return (int)zones_maj >= (int)nz - (int)fz; /* quorum.go:100-108 */
+    case PAXISIM_Q_FGRID_Q2:      return (int)zones_maj >= (int)fz + 1; /* quorum.go:111-119 */
+  }
+  return 0;
+}
+
+int oracle_quorum(uint32_t kind, uint32_t fz, uint32_t n_zones, const uint32_t* npz,
+                  uint32_t ack_mask) {
+  uint32_t zmask[PAXISIM_MAX_ZONES], z, r = 0, n = 0;
+  for (z = 0; z < n_zones; z++) {
+    zmask[z] = ((1u << npz[z]) - 1u) << r;
+    r += npz[z];
+  }
+  n = r;
+  return quorum_eval(kind, fz, n_zones, npz, zmask, n, ack_mask);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Simulation state                                                          */
+/* ------------------------------------------------------------------------ */
+typedef struct { uint32_t hdr, ballot, slot, cid; } rec_t;   /* 16-B message record */
+#define HDR(type, n) ((uint32_t)(type) | ((uint32_t)(n) << 8))
+#define HDR_TYPE(h) ((h) & 0xFFu)
+#define HDR_N(h) ((h) >> 8)
+
+/* log entry (paxos/paxos.go:11-18): ballot, command, request, quorum, commit */
+typedef struct { uint32_t ballot, cmd, req, meta; } entry_t;
+#define E_EXISTS 1u
+#define E_COMMIT 2u
+#define E_QUORUM 4u   /* quorum != nil */
+#define E_ACK(m) ((m) >> 16)
+
+/* a request = command id + who to reply to (message.go:24-30 NodeID/c) */
+#define REQ(cid, origin) ((uint32_t)(cid) | ((uint32_t)(origin) << 27))
+#define REQ_CID(q) ((q) & 0x07FFFFFFu)
+#define REQ_ORIGIN(q) ((q) >> 27)
+#define CID_MAX 0x07FFFFFFu
+
+#define PMAX 32
+#define FMAX 32
+#define CKI 16   /* checkpoint every CKI executed slots */
+#define CKR 8    /* checkpoints kept per replica */
+
+typedef struct replica {
+  /* paxos.Paxos fields (paxos/paxos.go:21-38) */
+  uint32_t ballot;
+  int32_t slot, execute;
+  uint32_t active;
+  uint32_t p1mask;                 /* p.quorum (phase 1) */
+  uint32_t npend, pend[PMAX];      /* p.requests */
+  entry_t* log;                    /* p.log, window [execute, execute+W) */
+  /* node.forwards (node.go:35, 165-172) */
+  uint32_t nfwd, fwd[FMAX];
+  /* socket fault state (socket.go:26-34), random process */
+  uint32_t drop_until[PAXISIM_MAX_N], slow_until[PAXISIM_MAX_N], slow_delay[PAXISIM_MAX_N];
+  /* executed-history digest + checkpoints */
+  uint64_t digest;
+  uint32_t ck_e[CKR];
+  uint64_t ck_d[CKR];
+  uint32_t flags;
+  uint32_t send_seq;
+  /* counters */
+  uint32_t delivered[PAXISIM_NMSG];
+  uint32_t client_requests, sent, dropped, discarded, commits, replies;
+  /* exec log (KATs) */
+  uint32_t* xlog;
+  uint32_t nx, capx;
+} replica_t;
+
+typedef struct cluster {
+  uint64_t gid, kc;
+  uint32_t poison_step;            /* first step at which a replica panicked */
+  uint32_t wk_cur[PAXISIM_MAX_WORKERS], wk_issued[PAXISIM_MAX_WORKERS];
+  replica_t rep[PAXISIM_MAX_N];
+  rec_t* mbox;                     /* [D][N][N+1][M] */
+  uint8_t* cnt;                    /* [D][N][N+1] */
+} cluster_t;
+
+struct oracle_sim {
+  paxisim_config cfg;
+  paxisim_workload wl;
+  paxisim_fault_process fp;
+  uint32_t N, Z, W, M, D, NS;      /* NS = N+1 sources (N = client) */
+  uint32_t zone_of[PAXISIM_MAX_N], node_of[PAXISIM_MAX_N], zmask[PAXISIM_MAX_ZONES];
+  paxisim_fault faults[PAXISIM_MAX_FAULTS];
+  uint32_t nfaults;
+  uint64_t C;
+  cluster_t* cl;
+  uint32_t t;                      /* next step to simulate */
+  int keep_xlog;
+};
+
+/* handler context: one replica of one cluster at one step */
+typedef struct ctx {
+  const struct oracle_sim* s;
+  cluster_t* c;
+  replica_t* p;
+  uint32_t r, t;
+  int stop;                        /* replica panicked in this step */
+} ctx_t;
+
+static inline rec_t* mb_rec(const struct oracle_sim* s, cluster_t* c, uint32_t b, uint32_t dst,
+                            uint32_t src, uint32_t k) {
+  return &c->mbox[(((size_t)b * s->N + dst) * s->NS + src) * s->M + k];
+}
+static inline uint8_t* mb_cnt(const struct oracle_sim* s, cluster_t* c, uint32_t b, uint32_t dst,
+                              uint32_t src) {
+  return &c->cnt[((size_t)b * s->N + dst) * s->NS + src];
+}
+
+static inline void raise_flag(ctx_t* x, uint32_t f) { x->p->flags |= f; }
+
+/* ------------------------------------------------------------------------ */
+/* Fault filter (socket.go:66-109): crash -> drop -> flaky -> slow           */
+/* ------------------------------------------------------------------------ */
+static int scripted(const struct oracle_sim* s, uint32_t kind, uint64_t gid, uint32_t src,
+                    uint32_t dst, uint32_t t, uint32_t* param) {
+  int hit = 0;
+  uint32_t i;
+  for (i = 0; i < s->nfaults; i++) {
+    const paxisim_fault* f = &s->faults[i];
+    if (f->kind != kind || f->src != src) continue;
+    if (kind != PAXISIM_FAULT_CRASH && f->dst != PAXISIM_ALL_DST && f->dst != dst) continue;
+    if (gid < f->cluster_lo || gid >= f->cluster_hi) continue;
+    if (t < f->step_from || t >= f->step_to) continue;
+    hit = 1;
+    if (param && f->param > *param) *param = f->param;
+  }
+  return hit;
+}
+static int crashed(const struct oracle_sim* s, const cluster_t* c, uint32_t r, uint32_t t) {
+  return scripted(s, PAXISIM_FAULT_CRASH, c->gid, r, 0, t, NULL);
+}
+
+/* socket.Send (socket.go:66-109) with the bucketed mailbox of DESIGN.md §3.2. */
+static void sock_send(ctx_t* x, uint32_t to, const rec_t* recs, uint32_t nrec) {
+  const struct oracle_sim* s = x->s;
+  replica_t* p = x->p;
+  uint32_t seq = p->send_seq++, delay = 0, flaky = 0, b;
+  uint8_t* cnt;
+  p->sent++;
+  if (to >= s->N) { p->dropped++; return; }                      /* unknown id: socket.go:86-88 */
+  if (crashed(s, x->c, x->r, x->t)) { p->dropped++; return; }    /* socket.go:69 */
+  if (x->t < p->drop_until[to] ||
+      scripted(s, PAXISIM_FAULT_DROP, x->c->gid, x->r, to, x->t, NULL)) { p->dropped++; return; } /* 73 */
+  if (scripted(s, PAXISIM_FAULT_FLAKY, x->c->gid, x->r, to, x->t, &flaky) && flaky > 0) {         /* 77-81 */
+    uint32_t u = (uint32_t)(draw(x->c->kc, x->t, TAG(PUR_FLAKY, x->r, seq)) >> 32);
+    if (ppm_hit(u, flaky)) { p->dropped++; return; }
+  }
+  if (x->t < p->slow_until[to]) delay = p->slow_delay[to];        /* 99-106 */
+  scripted(s, PAXISIM_FAULT_SLOW, x->c->gid, x->r, to, x->t, &delay);
+  if (delay > s->cfg.max_delay) delay = s->cfg.max_delay;
+  b = (x->t + 1u + delay) % s->D;
+  cnt = mb_cnt(s, x->c, b, to, x->r);
+  if ((uint32_t)*cnt + nrec > s->M) {                             /* bounded mailbox: lost */
+    raise_flag(x, PAXISIM_F_MBOX_OVF | PAXISIM_F_UNFAITHFUL);
+    p->dropped++;
+    return;
+  }
+  memcpy(mb_rec(s, x->c, b, to, x->r, *cnt), recs, nrec * sizeof(rec_t));
+  *cnt = (uint8_t)(*cnt + nrec);
+}
+
+static void send1(ctx_t* x, uint32_t to, uint32_t type, uint32_t ballot, uint32_t slot, uint32_t cid) {
+  rec_t m;
+  m.hdr = HDR(type, 0); m.ballot = ballot; m.slot = slot; m.cid = cid;
+  sock_send(x, to, &m, 1);
+}
+
+/* Broadcast: every peer except self, in IDs.Less order (socket.go:147-155; G1, G2) */
+static void broadcast1(ctx_t* x, uint32_t type, uint32_t ballot, uint32_t slot, uint32_t cid) {
+  uint32_t d;
+  for (d = 0; d < x->s->N; d++)
+    if (d != x->r) send1(x, d, type, ballot, slot, cid);
+}
+/* MulticastQuorum(q): the first q peers in ring order after self (socket.go:132-145; G8) */
+static void multicast_quorum1(ctx_t* x, uint32_t q, uint32_t type, uint32_t ballot, uint32_t slot,
+                              uint32_t cid) {
+  uint32_t i, sent = 0, N = x->s->N;
+  for (i = 1; i < N && sent < q; i++, sent++) send1(x, (x->r + i) % N, type, ballot, slot, cid);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Client (benchmark.go:246-275 worker; http.go:99 request path)            */
+/* ------------------------------------------------------------------------ */
+static void client_enqueue(ctx_t* x, uint32_t target, uint32_t cid) {
+  const struct oracle_sim* s = x->s;
+  uint32_t b = (x->t + 1u) % s->D;
+  uint8_t* cnt = mb_cnt(s, x->c, b, target, s->N);
+  rec_t* m;
+  if (*cnt >= s->M) { raise_flag(x, PAXISIM_F_MBOX_OVF | PAXISIM_F_UNFAITHFUL); return; }
+  m = mb_rec(s, x->c, b, target, s->N, *cnt);
+  m->hdr = HDR(PAXISIM_MSG_REQUEST, 0); m->ballot = 0; m->slot = 0; m->cid = cid;
+  (*cnt)++;
+}
+
+/* The HTTP response reaches worker w; it issues its next request. */
+static void client_reply(ctx_t* x, uint32_t cid) {
+  const struct oracle_sim* s = x->s;
+  uint32_t WK = s->wl.outstanding, w = (cid - 1u) % WK;
+  if (x->c->wk_cur[w] != cid) return;                /* duplicate reply: worker moved on */
+  x->p->replies++;
+  if (s->wl.max_requests == 0 || x->c->wk_issued[w] < s->wl.max_requests) {
+    uint64_t nc = 1ull + w + (uint64_t)WK * x->c->wk_issued[w];
+    if (nc > CID_MAX) { raise_flag(x, PAXISIM_F_PEND_OVF | PAXISIM_F_UNFAITHFUL); x->c->wk_cur[w] = 0; return; }
+    x->c->wk_issued[w]++;
+    x->c->wk_cur[w] = (uint32_t)nc;
+    client_enqueue(x, s->wl.target[w], (uint32_t)nc);
+  } else {
+    x->c->wk_cur[w] = 0;
+  }
+}
+
+/* Request.Reply (message.go:32-34): to the client, or back over the socket to
+ * the node the request came from (node.go:83-90 reply goroutine). */
+static void request_reply(ctx_t* x, uint32_t req, uint32_t reply_cmd) {
+  uint32_t o = REQ_ORIGIN(req);
+  if (o == PAXISIM_CLIENT_SRC) client_reply(x, REQ_CID(req));
+  else send1(x, o, PAXISIM_MSG_REPLY, 0, 0, reply_cmd);
+}
+
+/* node.Forward (node.go:165-172): remember the request, send it to id. */
+static void node_forward(ctx_t* x, uint32_t to, uint32_t req) {
+  replica_t* p = x->p;
+  uint32_t i, cid = REQ_CID(req);
+  for (i = 0; i < p->nfwd; i++)
+    if (REQ_CID(p->fwd[i]) == cid) break;
+  if (i == p->nfwd) {
+    if (p->nfwd == FMAX) raise_flag(x, PAXISIM_F_PEND_OVF | PAXISIM_F_UNFAITHFUL);
+    else p->fwd[p->nfwd++] = req;
+  } else {
+    p->fwd[i] = req;
+  }
+  send1(x, to, PAXISIM_MSG_REQUEST, 0, 0, cid);
+}
+
+/* node.recv Reply case (node.go:83-90): forwards[cmd].Reply(m). */
+static void handle_reply(ctx_t* x, uint32_t cid) {
+  replica_t* p = x->p;
+  uint32_t i;
+  for (i = 0; i < p->nfwd; i++)
+    if (REQ_CID(p->fwd[i]) == cid) break;
+  if (i == p->nfwd) {               /* Go: nil *Request (panic) or a retired entry */
+    raise_flag(x, PAXISIM_F_UNFAITHFUL);
+    return;
+  }
+  {
+    uint32_t req = p->fwd[i];
+    p->fwd[i] = p->fwd[--p->nfwd];  /* retire (bounded memory) */
+    request_reply(x, req, cid);
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Multi-Paxos (paxos/paxos.go, paxos/replica.go)                            */
+/* ------------------------------------------------------------------------ */
+static inline int in_window(const ctx_t* x, int32_t s) {
+  return s >= x->p->execute && s < x->p->execute + (int32_t)x->s->W;
+}
+static inline entry_t* log_at(const ctx_t* x, int32_t s) { return &x->p->log[(uint32_t)s & (x->s->W - 1u)]; }
+static inline int q1_ok(const ctx_t* x, uint32_t m) {
+  const struct oracle_sim* s = x->s;
+  return quorum_eval(s->cfg.q1, s->cfg.fz, s->Z, s->cfg.npz, s->zmask, s->N, m);
+}
+static inline int q2_ok(const ctx_t* x, uint32_t m) {
+  const struct oracle_sim* s = x->s;
+  return quorum_eval(s->cfg.q2, s->cfg.fz, s->Z, s->cfg.npz, s->zmask, s->N, m);
+}
+static inline int is_leader(const ctx_t* x) {             /* Paxos.IsLeader paxos.go:61-63 */
+  return x->p->active || bal_id(x->p->ballot) == x->r;
+}
+
+static void paxos_forward(ctx_t* x) {                     /* paxos.go:371-376 */
+  replica_t* p = x->p;
+  uint32_t i;
+  for (i = 0; i < p->npend; i++) node_forward(x, bal_id(p->ballot), p->pend[i]);
+  p->npend = 0;
+}
+
+static void paxos_p1a(ctx_t* x) {                         /* paxos.go:100-108 */
+  replica_t* p = x->p;
+  if (p->active) return;
+  if ((p->ballot >> 4) + 1u >= (1u << 27)) raise_flag(x, PAXISIM_F_BALLOT_OVF | PAXISIM_F_UNFAITHFUL);
+  p->ballot = bal_next(p->ballot, x->r);
+  p->p1mask = 1u << x->r;
+  broadcast1(x, PAXISIM_MSG_P1A, p->ballot, 0, 0);
+}
+
+static void paxos_p2a(ctx_t* x, uint32_t req) {           /* paxos.go:111-131 */
+  const struct oracle_sim* s = x->s;
+  replica_t* p = x->p;
+  p->slot++;
+  if (in_window(x, p->slot)) {
+    entry_t* e = log_at(x, p->slot);
+    e->ballot = p->ballot;
+    e->cmd = REQ_CID(req);
+    e->req = req;
+    e->meta = E_EXISTS | E_QUORUM | ((1u << x->r) << 16);
+  } else {
+    raise_flag(x, PAXISIM_F_WOVF | PAXISIM_F_UNFAITHFUL);  /* request lost */
+  }
+  if (s->cfg.thrifty) multicast_quorum1(x, s->N / 2 + 1, PAXISIM_MSG_P2A, p->ballot, (uint32_t)p->slot, REQ_CID(req));
+  else broadcast1(x, PAXISIM_MSG_P2A, p->ballot, (uint32_t)p->slot, REQ_CID(req));
+}
+
+static void paxos_handle_request(ctx_t* x, uint32_t req) { /* paxos.go:86-97 */
+  replica_t* p = x->p;
+  if (!p->active) {
+    if (p->npend == PMAX) raise_flag(x, PAXISIM_F_PEND_OVF | PAXISIM_F_UNFAITHFUL);
+    else p->pend[p->npend++] = req;
+    if (bal_id(p->ballot) != x->r) paxos_p1a(x);
+  } else {
+    paxos_p2a(x, req);
+  }
+}
+
+/* Replica.handleRequest (paxos/replica.go:42-66; read modes out of scope). */
+static void replica_handle_request(ctx_t* x, uint32_t req) {
+  if (x->s->cfg.ephemeral_leader || is_leader(x) || x->p->ballot == 0)
+    paxos_handle_request(x, req);
+  else
+    node_forward(x, bal_id(x->p->ballot), req);            /* `go r.Forward(...)` */
+}
+
+static void paxos_exec(ctx_t* x);
+
+static void paxos_handle_p1a(ctx_t* x, uint32_t mb) {      /* paxos.go:134-162 */
+  replica_t* p = x->p;
+  rec_t out[1 + PAXISIM_MAX_WINDOW];
+  uint32_t n = 0;
+  int32_t s, hi;
+  if (mb > p->ballot) {
+    p->ballot = mb;
+    p->active = 0;
+    paxos_forward(x);
+  }
+  if (p->flags & PAXISIM_F_WOVF) raise_flag(x, PAXISIM_F_UNFAITHFUL);  /* Go may hold skipped entries */
+  hi = p->slot;
+  if (hi > p->execute + (int32_t)x->s->W - 1) hi = p->execute + (int32_t)x->s->W - 1;
+  for (s = p->execute; s <= hi; s++) {
+    entry_t* e = log_at(x, s);
+    if (!(e->meta & E_EXISTS) || (e->meta & E_COMMIT)) continue;
+    n++;
+    out[n].hdr = HDR(PAXISIM_MSG_P1B_ENTRY, 0);
+    out[n].ballot = e->ballot;
+    out[n].slot = (uint32_t)s;
+    out[n].cid = e->cmd;
+  }
+  out[0].hdr = HDR(PAXISIM_MSG_P1B, n);
+  out[0].ballot = p->ballot;
+  out[0].slot = 0;
+  out[0].cid = 0;
+  sock_send(x, bal_id(mb), out, 1 + n);
+}
+
+static void paxos_update(ctx_t* x, const rec_t* log, uint32_t n) { /* paxos.go:164-180 */
+  replica_t* p = x->p;
+  uint32_t i;
+  for (i = 0; i < n; i++) {
+    int32_t s = (int32_t)log[i].slot;
+    if (s > p->slot) p->slot = s;
+    if (in_window(x, s)) {
+      entry_t* e = log_at(x, s);
+      if (e->meta & E_EXISTS) {
+        if (!(e->meta & E_COMMIT) && log[i].ballot > e->ballot) {
+          e->ballot = log[i].ballot;
+          e->cmd = log[i].cid;
+        }
+      } else {
+        e->ballot = log[i].ballot;
+        e->cmd = log[i].cid;
+        e->req = 0;
+        e->meta = E_EXISTS;                                /* quorum nil */
+      }
+    } else if (s < p->execute) {
+      raise_flag(x, PAXISIM_F_GHOST);
+    } else {
+      raise_flag(x, PAXISIM_F_WOVF);
+    }
+  }
+}
+
+static void paxos_handle_p1b(ctx_t* x, uint32_t src, uint32_t mb, const rec_t* log, uint32_t n) { /* paxos.go:183-230 */
+  replica_t* p = x->p;
+  if (mb < p->ballot || p->active) return;
+  paxos_update(x, log, n);
+  if (mb > p->ballot) {
+    p->ballot = mb;
+    p->active = 0;
+    paxos_forward(x);
+  }
+  if (bal_id(mb) == x->r && mb == p->ballot) {
+    p->p1mask |= 1u << src;
+    if (q1_ok(x, p->p1mask)) {
+      int32_t i, hi;
+      uint32_t k, npend;
+      uint32_t pend[PMAX];
+      p->active = 1;
+      if (p->flags & PAXISIM_F_WOVF) raise_flag(x, PAXISIM_F_UNFAITHFUL);
+      hi = p->slot;
+      if (hi > p->execute + (int32_t)x->s->W - 1) hi = p->execute + (int32_t)x->s->W - 1;
+      for (i = p->execute; i <= hi; i++) {
+        entry_t* e = log_at(x, i);
+        if (!(e->meta & E_EXISTS) || (e->meta & E_COMMIT)) continue;   /* nil gap skipped (G5) */
+        e->ballot = p->ballot;
+        e->meta = (e->meta & (E_EXISTS | E_COMMIT)) | E_QUORUM | ((1u << x->r) << 16);
+        broadcast1(x, PAXISIM_MSG_P2A, p->ballot, (uint32_t)i, e->cmd);
+      }
+      npend = p->npend;
+      memcpy(pend, p->pend, npend * sizeof(uint32_t));
+      p->npend = 0;
+      for (k = 0; k < npend; k++) paxos_p2a(x, pend[k]);
+    }
+  }
+}
+
+static void paxos_handle_p2a(ctx_t* x, uint32_t mb, int32_t ms, uint32_t mcid) { /* paxos.go:233-267 */
+  replica_t* p = x->p;
+  if (mb >= p->ballot) {
+    p->ballot = mb;
+    p->active = 0;
+    if (ms > p->slot) p->slot = ms;
+    if (in_window(x, ms)) {
+      entry_t* e = log_at(x, ms);
+      if (e->meta & E_EXISTS) {
+        if (!(e->meta & E_COMMIT) && mb > e->ballot) {
+          if (e->cmd != mcid && e->req) {
+            node_forward(x, bal_id(mb), e->req);
+            e->req = 0;
+          }
+          e->cmd = mcid;
+          e->ballot = mb;
+        }
+      } else {
+        e->ballot = mb;
+        e->cmd = mcid;
+        e->req = 0;
+        e->meta = E_EXISTS;
+      }
+    } else if (ms < p->execute) {
+      raise_flag(x, PAXISIM_F_GHOST);
+    } else {
+      raise_flag(x, PAXISIM_F_WOVF);
+    }
+  }
+  send1(x, bal_id(mb), PAXISIM_MSG_P2B, p->ballot, (uint32_t)ms, 0);
+}
+
+static void paxos_handle_p2b(ctx_t* x, uint32_t src, uint32_t mb, int32_t ms) { /* paxos.go:270-310 */
+  replica_t* p = x->p;
+  entry_t* e;
+  if (!in_window(x, ms)) {
+    if ((ms < p->execute && (p->flags & PAXISIM_F_GHOST)) ||
+        (ms >= p->execute && (p->flags & PAXISIM_F_WOVF)))
+      raise_flag(x, PAXISIM_F_UNFAITHFUL);
+    return;
+  }
+  e = log_at(x, ms);
+  if (!(e->meta & E_EXISTS) || mb < e->ballot || (e->meta & E_COMMIT)) return;
+  if (mb > p->ballot) {
+    p->ballot = mb;
+    p->active = 0;
+  }
+  if (bal_id(mb) == x->r && mb == e->ballot) {
+    if (!(e->meta & E_QUORUM)) {                           /* nil quorum: Go panics */
+      raise_flag(x, PAXISIM_F_POISON);
+      x->stop = 1;
+      return;
+    }
+    e->meta |= (1u << src) << 16;
+    if (q2_ok(x, E_ACK(e->meta))) {
+      e->meta |= E_COMMIT;
+      p->commits++;
+      broadcast1(x, PAXISIM_MSG_P3, mb, (uint32_t)ms, e->cmd);
+      if (x->s->cfg.reply_when_commit) {
+        if (!e->req) { raise_flag(x, PAXISIM_F_POISON); x->stop = 1; return; } /* nil r.Reply */
+        request_reply(x, e->req, REQ_CID(e->req));         /* Reply{Command: r.Command} */
+      } else {
+        paxos_exec(x);
+      }
+    }
+  }
+}
+
+static void paxos_handle_p3(ctx_t* x, uint32_t mb, int32_t ms, uint32_t mcid) { /* paxos.go:313-343 */
+  replica_t* p = x->p;
+  if (ms > p->slot) p->slot = ms;
+  if (in_window(x, ms)) {
+    entry_t* e = log_at(x, ms);
+    if (e->meta & E_EXISTS) {
+      if (e->cmd != mcid && e->req) {
+        node_forward(x, bal_id(mb), e->req);
+        e->req = 0;
+      }
+    } else {
+      e->ballot = 0;                                       /* &entry{} (G6) */
+      e->req = 0;
+      e->meta = E_EXISTS;
+    }
+    e->cmd = mcid;
+    e->meta |= E_COMMIT;
+    if (x->s->cfg.reply_when_commit) {
+      if (e->req) request_reply(x, e->req, REQ_CID(e->req));
+      return;
+    }
+  } else if (ms < p->execute) {
+    raise_flag(x, PAXISIM_F_GHOST);
+  } else {
+    raise_flag(x, PAXISIM_F_WOVF);
+  }
+  if (!x->s->cfg.reply_when_commit) paxos_exec(x);
+}
+
+static void paxos_exec(ctx_t* x) {                         /* paxos.go:345-369 */
+  replica_t* p = x->p;
+  for (;;) {
+    entry_t* e = log_at(x, p->execute);
+    if (!(e->meta & E_EXISTS) || !(e->meta & E_COMMIT)) break;
+    if (p->flags & PAXISIM_F_WOVF) raise_flag(x, PAXISIM_F_UNFAITHFUL);
+    if (e->req) {
+      request_reply(x, e->req, e->cmd);
+      e->req = 0;
+    }
+    p->digest = mix64(p->digest ^ (((uint64_t)(uint32_t)p->execute << 32) | e->cmd));
+    if (x->s->keep_xlog) {
+      if (p->nx == p->capx) {
+        p->capx = p->capx ? 2 * p->capx : 1024;
+        p->xlog = (uint32_t*)realloc(p->xlog, p->capx * sizeof(uint32_t));
+      }
+      p->xlog[p->nx++] = e->cmd;
+    }
+    e->meta = 0;                                           /* delete(p.log, p.execute) */
+    p->execute++;
+    if ((uint32_t)p->execute % CKI == 0) {
+      uint32_t k = ((uint32_t)p->execute / CKI) % CKR;
+      p->ck_e[k] = (uint32_t)p->execute;
+      p->ck_d[k] = p->digest;
+    }
+  }
+}
+
+/* node.handle dispatch (node.go:104-115) for one inbound message. */
+static void paxos_dispatch(ctx_t* x, uint32_t src, const rec_t* m) {
+  switch (HDR_TYPE(m->hdr)) {
+    case PAXISIM_MSG_REQUEST:
+      replica_handle_request(x, REQ(m->cid, src == x->s->N ? PAXISIM_CLIENT_SRC : src));
+      break;
+    case PAXISIM_MSG_REPLY: handle_reply(x, m->cid); break;
+    case PAXISIM_MSG_P1A: paxos_handle_p1a(x, m->ballot); break;
+    case PAXISIM_MSG_P1B: paxos_handle_p1b(x, src, m->ballot, m + 1, HDR_N(m->hdr)); break;
+    case PAXISIM_MSG_P2A: paxos_handle_p2a(x, m->ballot, (int32_t)m->slot, m->cid); break;
+    case PAXISIM_MSG_P2B: paxos_handle_p2b(x, src, m->ballot, (int32_t)m->slot); break;
+    case PAXISIM_MSG_P3: paxos_handle_p3(x, m->ballot, (int32_t)m->slot, m->cid); break;
+    default: break;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* One replica, one step                                    */
+/* ------------------------------------------------------------------------ */
+static void fault_process(ctx_t* x) {
+  const struct oracle_sim* s = x->s;
+  const paxisim_fault_process* fp = &s->fp;
+  replica_t* p = x->p;
+  uint32_t d;
+  if (fp->drop_ppm == 0 && fp->slow_ppm == 0) return;
+  for (d = 0; d < s->N; d++) {
+    uint64_t u;
+    if (d == x->r) continue;
+    u = draw(x->c->kc, x->t, TAG(PUR_LINK, x->r, d));
+    if (fp->drop_ppm && x->t >= p->drop_until[d] && ppm_hit((uint32_t)u, fp->drop_ppm))
+      p->drop_until[d] = x->t + fp->drop_len;
+    if (fp->slow_ppm && x->t >= p->slow_until[d] && ppm_hit((uint32_t)(u >> 32), fp->slow_ppm)) {
+      uint32_t span = fp->slow_max - fp->slow_min + 1u;
+      uint32_t v = (uint32_t)(draw(x->c->kc, x->t, TAG(PUR_SLOWD, x->r, d)) >> 32);
+      p->slow_until[d] = x->t + fp->slow_len;
+      p->slow_delay[d] = fp->slow_min + (uint32_t)(((uint64_t)v * span) >> 32);
+    }
+  }
+}
+
+static void replica_step(const struct oracle_sim* s, cluster_t* c, uint32_t r, uint32_t t) {
+  ctx_t x;
+  uint32_t b = t % s->D, src, rem[PAXISIM_MAX_N + 1], pos[PAXISIM_MAX_N + 1], total = 0, i;
+  int crash;
+  x.s = s; x.c = c; x.p = &c->rep[r]; x.r = r; x.t = t; x.stop = 0;
+  x.p->send_seq = 0;
+  fault_process(&x);
+  crash = crashed(s, c, r, t);
+  for (src = 0; src < s->NS; src++) {
+    rem[src] = *mb_cnt(s, c, b, r, src);
+    pos[src] = 0;
+    if (crash && src < s->N && rem[src]) {               /* socket.Recv discards (socket.go:111-118) */
+      uint32_t k = 0;
+      while (k < rem[src]) {
+        rec_t* m = mb_rec(s, c, b, r, src, k);
+        x.p->discarded++;
+        k += 1u + (HDR_TYPE(m->hdr) == PAXISIM_MSG_P1B ? HDR_N(m->hdr) : 0u);
+      }
+      rem[src] = 0;
+    }
+    total += rem[src];
+  }
+  for (i = 0; total > 0 && !x.stop; i++) {
+    uint32_t u = (uint32_t)(draw(c->kc, t, TAG(PUR_ORDER, r, i)) >> 32);
+    uint32_t pick = (uint32_t)(((uint64_t)u * total) >> 32), len;
+    rec_t* m;
+    for (src = 0; pick >= rem[src]; src++) pick -= rem[src];
+    m = mb_rec(s, c, b, r, src, pos[src]);
+    len = 1u + (HDR_TYPE(m->hdr) == PAXISIM_MSG_P1B ? HDR_N(m->hdr) : 0u);
+    pos[src] += len;
+    rem[src] -= len;
+    total -= len;
+    if (src == s->N) x.p->client_requests++;
+    else x.p->delivered[HDR_TYPE(m->hdr)]++;
+    paxos_dispatch(&x, src, m);
+  }
+  for (src = 0; src < s->NS; src++) *mb_cnt(s, c, b, r, src) = 0;
+  if (x.stop && c->poison_step > t) c->poison_step = t;
+}
+
+static void cluster_step(const struct oracle_sim* s, cluster_t* c, uint32_t t) {
+  uint32_t r;
+  if (c->poison_step < t) return;                          /* a panic froze the process */
+  for (r = 0; r < s->N; r++) replica_step(s, c, r, t);
+}
+
+/* ------------------------------------------------------------------------ */
+/* API                                                                       */
+/* ------------------------------------------------------------------------ */
+static int check_config(const paxisim_config* cfg, const paxisim_workload* wl,
+                        const paxisim_fault_process* fp, uint32_t* N_out) {
+  uint32_t z, N = 0, w;
+  if (cfg->protocol != PAXISIM_PAXOS) return fail(PAXISIM_EUNSUPP, "protocol %u not built", cfg->protocol);
+  if (cfg->n_zones < 1 || cfg->n_zones > PAXISIM_MAX_ZONES) return fail(PAXISIM_EINVAL, "n_zones");
+  for (z = 0; z < cfg->n_zones; z++) {
+    if (cfg->npz[z] < 1) return fail(PAXISIM_EINVAL, "npz[%u] must be >= 1", z);
+    N += cfg->npz[z];
+  }
+  if (N < 1 || N > PAXISIM_MAX_N) return fail(PAXISIM_EINVAL, "N=%u out of range", N);
+  if (cfg->window < 8 || cfg->window > PAXISIM_MAX_WINDOW || (cfg->window & (cfg->window - 1)))
+    return fail(PAXISIM_EINVAL, "window must be a power of 2 in [8,64]");
+  if (cfg->mbox_cap < 2 || cfg->mbox_cap > PAXISIM_MAX_MBOX) return fail(PAXISIM_EINVAL, "mbox_cap");
+  if (cfg->max_delay > PAXISIM_MAX_DELAY) return fail(PAXISIM_EINVAL, "max_delay");
+  if (cfg->q1 > PAXISIM_Q_FGRID_Q2 || cfg->q2 > PAXISIM_Q_FGRID_Q2) return fail(PAXISIM_EINVAL, "quorum kind");
+  if (cfg->clusters < 1) return fail(PAXISIM_EINVAL, "clusters");
+  if (wl->outstanding < 1 || wl->outstanding > PAXISIM_MAX_WORKERS) return fail(PAXISIM_EINVAL, "outstanding");
+  if (wl->outstanding > cfg->mbox_cap) return fail(PAXISIM_EINVAL, "outstanding exceeds mbox_cap");
+  for (w = 0; w < wl->outstanding; w++)
+    if (wl->target[w] >= N) return fail(PAXISIM_EINVAL, "target[%u]", w);
+  if (fp->slow_ppm && (fp->slow_min > fp->slow_max || fp->slow_max > cfg->max_delay))
+    return fail(PAXISIM_EINVAL, "slow delay range exceeds max_delay");
+  *N_out = N;
+  return 0;
+}
+
+static void cluster_init(struct oracle_sim* s, cluster_t* c, uint64_t gid, entry_t* logs) {
+  uint32_t r, w;
+  memset(c->rep, 0, sizeof c->rep);
+  c->gid = gid;
+  c->kc = cluster_key(s->cfg.seed, gid);
+  c->poison_step = 0xFFFFFFFFu;
+  for (r = 0; r < s->N; r++) {
+    c->rep[r].slot = -1;                                   /* paxos.go:45 */
+    c->rep[r].log = logs + (size_t)r * s->W;
+  }
+  memset(c->wk_cur, 0, sizeof c->wk_cur);
+  memset(c->wk_issued, 0, sizeof c->wk_issued);
+  /* every worker's first request waits at its target at step 0 */
+  for (w = 0; w < s->wl.outstanding; w++) {
+    uint32_t tg = s->wl.target[w];
+    uint8_t* cnt = mb_cnt(s, c, 0, tg, s->N);
+    rec_t* m = mb_rec(s, c, 0, tg, s->N, *cnt);
+    m->hdr = HDR(PAXISIM_MSG_REQUEST, 0); m->ballot = 0; m->slot = 0; m->cid = 1u + w;
+    (*cnt)++;
+    c->wk_cur[w] = 1u + w;
+    c->wk_issued[w] = 1;
+  }
+}
+
+int oracle_create(const paxisim_config* cfg, const paxisim_workload* wl,
+                  const paxisim_fault_process* fp, oracle_sim** out) {
+  struct oracle_sim* s;
+  uint32_t N = 0, z, r = 0;
+  uint64_t i;
+  paxisim_fault_process nofp;
+  int rc;
+  if (!cfg || !wl || !out) return fail(PAXISIM_EINVAL, "null argument");
+  if (!fp) { memset(&nofp, 0, sizeof nofp); fp = &nofp; }
+  if ((rc = check_config(cfg, wl, fp, &N))) return rc;
+  s = (struct oracle_sim*)calloc(1, sizeof *s);
+  if (!s) return fail(PAXISIM_ENOMEM, "oom");
+  s->cfg = *cfg; s->wl = *wl; s->fp = *fp;
+  s->N = N; s->Z = cfg->n_zones; s->W = cfg->window; s->M = cfg->mbox_cap;
+  s->D = cfg->max_delay + 2u; s->NS = N + 1u;
+  if (s->wl.outstanding > PAXISIM_MAX_WORKERS) s->wl.outstanding = PAXISIM_MAX_WORKERS;
+  for (z = 0; z < s->Z; z++) {
+    uint32_t k;
+    s->zmask[z] = ((1u << cfg->npz[z]) - 1u) << r;
+    for (k = 0; k < cfg->npz[z]; k++, r++) { s->zone_of[r] = z + 1; s->node_of[r] = k + 1; }
+  }
+  s->C = cfg->clusters;
+  s->keep_xlog = cfg->clusters <= 16;
+  s->cl = (cluster_t*)calloc(s->C, sizeof(cluster_t));
+  if (!s->cl) { free(s); return fail(PAXISIM_ENOMEM, "oom clusters"); }
+  for (i = 0; i < s->C; i++) {
+    cluster_t* c = &s->cl[i];
+    entry_t* logs = (entry_t*)calloc((size_t)N * s->W, sizeof(entry_t));
+    c->mbox = (rec_t*)malloc((size_t)s->D * N * s->NS * s->M * sizeof(rec_t));
+    c->cnt = (uint8_t*)calloc((size_t)s->D * N * s->NS, 1);
+    if (!logs || !c->mbox || !c->cnt) { s->C = i + 1; oracle_destroy(s); return fail(PAXISIM_ENOMEM, "oom"); }
+    cluster_init(s, c, cfg->cluster_base + i, logs);
+  }
+  *out = s;
+  return 0;
+}
+
+int oracle_destroy(oracle_sim* s) {
+  uint64_t i;
+  uint32_t r;
+  if (!s) return 0;
+  for (i = 0; i < s->C; i++) {
+    cluster_t* c = &s->cl[i];
+    if (c->rep[0].log) free(c->rep[0].log);
+    for (r = 0; r < s->N; r++) free(c->rep[r].xlog);
+    free(c->mbox);
+    free(c->cnt);
+  }
+  free(s->cl);
+  free(s);
+  return 0;
+}
+
+int oracle_fault_add(oracle_sim* s, const paxisim_fault* f) {
+  if (!s || !f) return fail(PAXISIM_EINVAL, "null argument");
+  if (s->nfaults == PAXISIM_MAX_FAULTS) return fail(PAXISIM_EINVAL, "fault table full");
+  if (f->kind > PAXISIM_FAULT_CRASH || f->src >= s->N ||
+      (f->dst != PAXISIM_ALL_DST && f->dst >= s->N))
+    return fail(PAXISIM_EINVAL, "bad fault");
+  if (f->kind == PAXISIM_FAULT_SLOW && f->param > s->cfg.max_delay)
+    return fail(PAXISIM_EINVAL, "slow delay exceeds max_delay");
+  s->faults[s->nfaults++] = *f;
+  return 0;
+}
+
+typedef struct { struct oracle_sim* s; uint64_t lo, hi; uint32_t t0, n; } shard_t;
+static void* run_shard(void* a) {
+  shard_t* sh = (shard_t*)a;
+  uint64_t i;
+  uint32_t k;
+  for (i = sh->lo; i < sh->hi; i++)
+    for (k = 0; k < sh->n; k++) cluster_step(sh->s, &sh->s->cl[i], sh->t0 + k);
+  return NULL;
+}
+
+int oracle_step(oracle_sim* s, uint32_t nsteps, int nthreads) {
+  if (!s) return fail(PAXISIM_EINVAL, "null handle");
+  if (nthreads <= 1) {
+    shard_t sh = {s, 0, s->C, s->t, nsteps};
+    run_shard(&sh);
+  } else {
+    pthread_t th[256];
+    shard_t sh[256];
+    int k;
+    if (nthreads > 256) nthreads = 256;
+    for (k = 0; k < nthreads; k++) {
+      sh[k].s = s; sh[k].t0 = s->t; sh[k].n = nsteps;
+      sh[k].lo = s->C * (uint64_t)k / (uint64_t)nthreads;
+      sh[k].hi = s->C * (uint64_t)(k + 1) / (uint64_t)nthreads;
+      pthread_create(&th[k], NULL, run_shard, &sh[k]);
+    }
+    for (k = 0; k < nthreads; k++) pthread_join(th[k], NULL);
+  }
+  s->t += nsteps;
+  return 0;
+}
+
+static void fill_state(const struct oracle_sim* s, const cluster_t* c, uint32_t r,
+                       paxisim_replica_state* o) {
+  const replica_t* p = &c->rep[r];
+  uint32_t rid = bal_id(p->ballot);
+  memset(o, 0, sizeof *o);
+  o->ballot = p->ballot ? oracle_new_ballot(p->ballot >> 4, s->zone_of[rid], s->node_of[rid]) : 0;
+  o->slot = p->slot;
+  o->execute = p->execute;
+  o->active = p->active;
+  o->flags = p->flags;
+  o->digest = p->digest;
+  o->p1_acks = p->p1mask;
+  o->npending = p->npend;
+  memcpy(o->delivered, p->delivered, sizeof o->delivered);
+  o->client_requests = p->client_requests;
+  o->sent = p->sent;
+  o->dropped = p->dropped;
+  o->discarded = p->discarded;
+  o->commits = p->commits;
+  o->replies = p->replies;
+}
+
+int oracle_read_state(oracle_sim* s, uint64_t lo, uint64_t n, paxisim_replica_state* out) {
+  uint64_t i;
+  uint32_t r;
+  if (!s || !out) return fail(PAXISIM_EINVAL, "null argument");
+  if (lo + n > s->C) return fail(PAXISIM_ERANGE, "cluster range");
+  for (i = 0; i < n; i++)
+    for (r = 0; r < s->N; r++) fill_state(s, &s->cl[lo + i], r, &out[i * s->N + r]);
+  return 0;
+}
+
+int oracle_stats_get(oracle_sim* s, paxisim_stats* o) {
+  uint64_t i;
+  uint32_t r, k;
+  if (!s || !o) return fail(PAXISIM_EINVAL, "null argument");
+  memset(o, 0, sizeof *o);
+  o->steps = s->t;
+  o->clusters = s->C;
+  for (i = 0; i < s->C; i++) {
+    uint32_t cf = 0;
+    for (r = 0; r < s->N; r++) {
+      const replica_t* p = &s->cl[i].rep[r];
+      for (k = 0; k < PAXISIM_NMSG; k++) {
+        o->delivered[k] += p->delivered[k];
+        o->delivered_total += p->delivered[k];
+      }
+      o->client_requests += p->client_requests;
+      o->sent += p->sent;
+      o->dropped += p->dropped;
+      o->discarded += p->discarded;
+      o->commits += p->commits;
+      o->replies += p->replies;
+      cf |= p->flags;
+    }
+    for (k = 0; k < 8; k++) if (cf & (1u << k)) o->flagged[k]++;
+  }
+  return 0;
+}
+
+/* Agreement scan (client.go:279-320 per-index set size <= 1; tla Safety):
+ * checkpoints of the executed-history digest must agree across replicas. */
+int oracle_check(oracle_sim* s, uint64_t* violations) {
+  uint64_t i, v = 0;
+  uint32_t a, b, k, j;
+  if (!s || !violations) return fail(PAXISIM_EINVAL, "null argument");
+  for (i = 0; i < s->C; i++) {
+    const cluster_t* c = &s->cl[i];
+    int bad = 0;
+    for (a = 0; a < s->N && !bad; a++)
+      for (b = a + 1; b < s->N && !bad; b++) {
+        const replica_t *p = &c->rep[a], *q = &c->rep[b];
+        if (p->execute == q->execute && p->digest != q->digest) bad = 1;
+        for (k = 0; k < CKR && !bad; k++)
+          for (j = 0; j < CKR && !bad; j++)
+            if (p->ck_e[k] && p->ck_e[k] == q->ck_e[j] && p->ck_d[k] != q->ck_d[j]) bad = 1;
+      }
+    v += (uint64_t)bad;
+  }
+  *violations = v;
+  return 0;
+}
+
+int oracle_exec_log(oracle_sim* s, uint64_t cl, uint32_t r, uint32_t* buf, uint32_t cap, uint32_t* n_out) {
+  const replica_t* p;
+  uint32_t n;
+  if (!s || !n_out || cl >= s->C || r >= s->N) return fail(PAXISIM_EINVAL, "bad argument");
+  if (!s->keep_xlog) return fail(PAXISIM_EUNSUPP, "exec log kept only for <= 16 clusters");
+  p = &s->cl[cl].rep[r];
+  n = p->nx < cap ? p->nx : cap;
+  if (buf && n) memcpy(buf, p->xlog, n * sizeof(uint32_t));
+  *n_out = p->nx;
+  return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Linearizability checker (checker.go:11-104, lib/graph.go:180-232)         */
+/* Vertex iteration is in insertion order (Go's map order is random; the     */
+/* reference's KATs do not depend on it).                                    */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  int n;
+  int64_t *hin, *in, *hout, *out, *start, *end;
+  unsigned char* present;    /* vertex in graph */
+  int* order;                /* insertion order of vertices */
+  int norder;
+  unsigned char* adj;        /* adj[u*n+v]: edge u -> v */
+} lgraph_t;
+
+static int lg_has(lgraph_t* g, int v) { return g->present[v]; }
+static void lg_add(lgraph_t* g, int v) {
+  if (g->present[v]) return;
+  g->present[v] = 1;
+  g->order[g->norder++] = v;
+}
+static void lg_remove(lgraph_t* g, int v) {
+  int i, k = 0;
+  if (!g->present[v]) return;
+  g->present[v] = 0;
+  for (i = 0; i < g->n; i++) { g->adj[v * g->n + i] = 0; g->adj[i * g->n + v] = 0; }
+  for (i = 0; i < g->norder; i++) if (g->order[i] != v) g->order[k++] = g->order[i];
+  g->norder = k;
+}
+static void lg_edge(lgraph_t* g, int u, int v) {
+  lg_add(g, u);
+  lg_add(g, v);
+  g->adj[u * g->n + v] = 1;
+}
+static int happen_before(lgraph_t* g, int a, int b) { return g->end[a] < g->start[b]; } /* operation.go:12-14 */
+static void chk_add(lgraph_t* g, int o) {                 /* checker.go:21-33 */
+  int i;
+  if (lg_has(g, o)) return;
+  lg_add(g, o);
+  for (i = 0; i < g->norder; i++) {
+    int v = g->order[i];
+    if (happen_before(g, v, o)) lg_edge(g, v, o);
+  }
+}
+/* graph.go:180-193 visit; returns 1 if a cycle is found, gray marks the stack */
+static int lg_visit(lgraph_t* g, int v, unsigned char* color) {
+  int i;
+  color[v] = 1;
+  for (i = 0; i < g->norder; i++) {
+    int u = g->order[i];
+    if (!g->adj[v * g->n + u]) continue;
+    if (color[u] == 1) return 1;
+    if (color[u] == 0 && lg_visit(g, u, color)) return 1;
+  }
+  color[v] = 2;
+  return 0;
+}
+
+int oracle_linearizable(const int64_t* ops, int n) {
+  lgraph_t g;
+  int *idx, i, j, anomalies = 0;
+  unsigned char* color;
+  if (n <= 0) return 0;
+  memset(&g, 0, sizeof g);
+  g.n = n;
+  g.hin = (int64_t*)malloc(6 * (size_t)n * sizeof(int64_t));
+  if (!g.hin) return -1;
+  g.in = g.hin + n; g.hout = g.in + n; g.out = g.hout + n; g.start = g.out + n; g.end = g.start + n;
+  g.present = (unsigned char*)calloc((size_t)n, 1);
+  g.order = (int*)malloc((size_t)n * sizeof(int));
+  g.adj = (unsigned char*)calloc((size_t)n * n, 1);
+  idx = (int*)malloc((size_t)n * sizeof(int));
+  color = (unsigned char*)malloc((size_t)n);
+  /* sort.Sort(byTime(history)): stable by start (insertion sort for small n) */
+  for (i = 0; i < n; i++) idx[i] = i;
+  for (i = 1; i < n; i++) {
+    int v = idx[i], k = i - 1;
+    while (k >= 0 && ops[6 * idx[k] + 4] > ops[6 * v + 4]) { idx[k + 1] = idx[k]; k--; }
+    idx[k + 1] = v;
+  }
+  for (i = 0; i < n; i++) {
+    const int64_t* o = &ops[6 * idx[i]];
+    g.hin[i] = o[0]; g.in[i] = o[1]; g.hout[i] = o[2]; g.out[i] = o[3]; g.start[i] = o[4]; g.end[i] = o[5];
+  }
+  for (i = 0; i < n; i++) {                                 /* checker.go:73-102 */
+    chk_add(&g, i);
+    if (!g.hin[i]) {                                        /* read */
+      int match = -1, k;
+      for (j = i + 1; j < n && !happen_before(&g, i, j) && !happen_before(&g, j, i); j++)
+        if (!g.hout[j]) chk_add(&g, j);                     /* look-ahead concurrent writes */
+      for (k = 0; k < g.norder; k++) {                      /* match: checker.go:44-52 */
+        int v = g.order[k];
+        if (g.hin[v] == g.hout[i] && (!g.hout[i] || g.in[v] == g.out[i])) { match = v; break; }
+      }
+      if (match >= 0) {                                     /* merge: checker.go:55-67 */
+        for (k = 0; k < g.norder; k++) {
+          int s2 = g.order[k];
+          if (g.adj[s2 * n + i] && s2 != match) lg_edge(&g, s2, match);
+        }
+        if (g.end[i] < g.end[match]) g.end[match] = g.end[i];
+        lg_remove(&g, i);
+      }
+      {                                                     /* Cycle: graph.go:212-232 */
+        int found = 0;
+        memset(color, 0, (size_t)n);
+        for (k = 0; k < g.norder && !found; k++)
+          if (color[g.order[k]] == 0 && lg_visit(&g, g.order[k], color)) found = 1;
+        if (found) {
+          int a, b;
+          anomalies++;
+          for (a = 0; a < g.norder; a++)
+            for (b = 0; b < g.norder; b++) {
+              int u = g.order[a], v = g.order[b];
+              if (color[u] == 1 && color[v] == 1 && g.adj[u * n + v] && g.start[u] > g.end[v])
+                g.adj[u * n + v] = 0;
+            }
+        }
+      }
+    }
+  }
+  free(g.hin); free(g.present); free(g.order); free(g.adj); free(idx); free(color);
+  return anomalies;
+}

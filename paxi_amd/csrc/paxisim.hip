@@ -1,0 +1,486 @@
+// paxisim.hip — C-ABI (include/paxisim.h) over the gfx950 simulation kernels.
+//
+// Product path: everything here runs on the GPU.  There is no CPU fallback;
+// a handle whose device cannot be initialised fails paxisim_create with
+// PAXISIM_EDEVICE.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "paxisim_dev.h"
+#include "paxos_kernel.h"
+
+using namespace pxs;
+
+static thread_local char g_err[512];
+static int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+  return code;
+}
+#define HIPCHK(expr)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      return fail(PAXISIM_EDEVICE, "%s failed: %s", #expr, hipGetErrorString(e_));    \
+  } while (0)
+
+struct paxisim {
+  paxisim_config cfg;
+  paxisim_workload wl;
+  paxisim_fault_process fp;
+  Params P;
+  uint32_t zone_of[PAXISIM_MAX_N], node_of[PAXISIM_MAX_N];
+  std::vector<paxisim_fault> faults;
+  paxisim_fault* d_faults = nullptr;
+  void* arena = nullptr;
+  size_t arena_bytes = 0;
+  uint64_t* d_scratch = nullptr;   // reductions
+  hipStream_t stream = nullptr;
+  uint32_t t = 0;
+  uint32_t S = 32;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
+  double kernel_ms = 0;
+  uint64_t launches = 0;
+};
+
+extern "C" int paxisim_abi_version(void) { return PAXISIM_ABI_VERSION; }
+extern "C" const char* paxisim_last_error(void) { return g_err; }
+
+// ---------------------------------------------------------------------------
+// kernels: init, stats reduction, state gather, agreement scan
+// ---------------------------------------------------------------------------
+__global__ void init_kernel(Params P) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= P.C) return;
+  P.kc[c] = cluster_key(P.seed, P.cluster_base + c);
+  P.poison[c] = 0xFFFFFFFFu;
+  for (uint32_t r = 0; r < P.N; r++) P.slot[rc(P, r, c)] = 0xFFFFFFFFu;   // slot: -1 (paxos.go:45)
+  if (c >= P.clusters) return;
+  for (uint32_t w = 0; w < P.WK; w++) {         // each worker's first request waits at step 0
+    const size_t bx = box(P, 0, P.target[w], P.N);
+    uint8_t* cp = cnt_at(P, bx, c);
+    *rec_at(P, bx, *cp, c) = make_uint4(PAXISIM_MSG_REQUEST, 0u, 0u, 1u + w);
+    *cp = (uint8_t)(*cp + 1u);
+    P.wk_cur[(size_t)w * P.C + c] = 1u + w;
+    P.wk_issued[(size_t)w * P.C + c] = 1u;
+  }
+}
+
+constexpr int NRED = NSTAT + 8;   // counters + flagged bits
+
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  return v;
+}
+
+__global__ void stats_kernel(Params P, uint64_t* out) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = c < P.clusters;
+  uint32_t cf = 0;
+  for (int k = 0; k < NSTAT; k++) {
+    uint64_t v = 0;
+    if (live)
+      for (uint32_t r = 0; r < P.N; r++) v += P.stats[krc(P, k, r, c)];
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd((unsigned long long*)&out[k], (unsigned long long)v);
+  }
+  if (live)
+    for (uint32_t r = 0; r < P.N; r++) cf |= P.flags[rc(P, r, c)];
+  for (int b = 0; b < 8; b++) {
+    uint64_t v = wave_sum((cf >> b) & 1u);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd((unsigned long long*)&out[NSTAT + b], (unsigned long long)v);
+  }
+}
+
+__global__ void gather_kernel(Params P, uint64_t lo, uint64_t n, paxisim_replica_state* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * P.N) return;
+  const uint64_t c = lo + i / P.N;
+  const uint32_t r = (uint32_t)(i % P.N);
+  const size_t j = rc(P, r, c);
+  paxisim_replica_state s;
+  memset(&s, 0, sizeof s);
+  s.ballot = P.ballot[j];             // compressed; expanded on the host
+  s.slot = (int32_t)P.slot[j];
+  s.execute = (int32_t)P.execute[j];
+  s.active = P.meta[j] & 1u;
+  s.p1_acks = P.meta[j] >> 16;
+  s.flags = P.flags[j];
+  s.digest = P.digest[j];
+  s.npending = P.npend[j];
+  for (int k = 0; k < PAXISIM_NMSG; k++) s.delivered[k] = P.stats[krc(P, ST_DELIV0 + k, r, c)];
+  s.client_requests = P.stats[krc(P, ST_CLIENT, r, c)];
+  s.sent = P.stats[krc(P, ST_SENT, r, c)];
+  s.dropped = P.stats[krc(P, ST_DROPPED, r, c)];
+  s.discarded = P.stats[krc(P, ST_DISCARDED, r, c)];
+  s.commits = P.stats[krc(P, ST_COMMITS, r, c)];
+  s.replies = P.stats[krc(P, ST_REPLIES, r, c)];
+  out[i] = s;
+}
+
+// Agreement scan (client.go:279-320; tla/wpaxos.tla Safety): replicas that
+// executed the same number of slots must hold the same digest, and digest
+// checkpoints taken at the same executed count must agree.
+__global__ void check_kernel(Params P, uint64_t* out) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t bad = 0;
+  if (c < P.clusters) {
+    for (uint32_t a = 0; a < P.N && !bad; a++)
+      for (uint32_t b = a + 1; b < P.N && !bad; b++) {
+        if (P.execute[rc(P, a, c)] == P.execute[rc(P, b, c)] && P.digest[rc(P, a, c)] != P.digest[rc(P, b, c)])
+          bad = 1;
+        for (uint32_t k = 0; k < CKR && !bad; k++) {
+          const uint32_t ea = P.ck_e[krc(P, k, a, c)];
+          if (!ea) continue;
+          for (uint32_t j = 0; j < CKR && !bad; j++)
+            if (P.ck_e[krc(P, j, b, c)] == ea && P.ck_d[krc(P, k, a, c)] != P.ck_d[krc(P, j, b, c)]) bad = 1;
+        }
+      }
+  }
+  bad = wave_sum(bad);
+  if ((threadIdx.x & 63) == 0 && bad) atomicAdd((unsigned long long*)out, (unsigned long long)bad);
+}
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+static int check_config(const paxisim_config* cfg, const paxisim_workload* wl, const paxisim_fault_process* fp,
+                        uint32_t* N_out) {
+  uint32_t N = 0;
+  if (cfg->protocol != PAXISIM_PAXOS) return fail(PAXISIM_EUNSUPP, "protocol %u not built", cfg->protocol);
+  if (cfg->n_zones < 1 || cfg->n_zones > PAXISIM_MAX_ZONES) return fail(PAXISIM_EINVAL, "n_zones");
+  for (uint32_t z = 0; z < cfg->n_zones; z++) {
+    if (cfg->npz[z] < 1) return fail(PAXISIM_EINVAL, "npz[%u] must be >= 1", z);
+    N += cfg->npz[z];
+  }
+  if (N < 1 || N > PAXISIM_MAX_N) return fail(PAXISIM_EINVAL, "N=%u out of range", N);
+  if (cfg->window < 8 || cfg->window > PAXISIM_MAX_WINDOW || (cfg->window & (cfg->window - 1)))
+    return fail(PAXISIM_EINVAL, "window must be a power of 2 in [8,64]");
+  if (cfg->mbox_cap < 2 || cfg->mbox_cap > PAXISIM_MAX_MBOX) return fail(PAXISIM_EINVAL, "mbox_cap");
+  if (cfg->max_delay > PAXISIM_MAX_DELAY) return fail(PAXISIM_EINVAL, "max_delay");
+  if (cfg->q1 > PAXISIM_Q_FGRID_Q2 || cfg->q2 > PAXISIM_Q_FGRID_Q2) return fail(PAXISIM_EINVAL, "quorum kind");
+  if (cfg->clusters < 1) return fail(PAXISIM_EINVAL, "clusters");
+  if (wl->outstanding < 1 || wl->outstanding > PAXISIM_MAX_WORKERS) return fail(PAXISIM_EINVAL, "outstanding");
+  if (wl->outstanding > cfg->mbox_cap) return fail(PAXISIM_EINVAL, "outstanding exceeds mbox_cap");
+  for (uint32_t w = 0; w < wl->outstanding; w++)
+    if (wl->target[w] >= N) return fail(PAXISIM_EINVAL, "target[%u]", w);
+  if (fp->slow_ppm && (fp->slow_min > fp->slow_max || fp->slow_max > cfg->max_delay))
+    return fail(PAXISIM_EINVAL, "slow delay range exceeds max_delay");
+  *N_out = N;
+  return 0;
+}
+
+template <typename T>
+static T* carve(char*& p, size_t count) {
+  T* out = reinterpret_cast<T*>(p);
+  p += (count * sizeof(T) + 255) & ~size_t(255);
+  return out;
+}
+
+static int flush_events(paxisim* h) {
+  for (auto& e : h->evs) {
+    float ms = 0;
+    HIPCHK(hipEventSynchronize(e.second));
+    HIPCHK(hipEventElapsedTime(&ms, e.first, e.second));
+    h->kernel_ms += ms;
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  h->evs.clear();
+  return 0;
+}
+
+extern "C" int paxisim_destroy(paxisim* h) {
+  if (!h) return 0;
+  (void)hipSetDevice(h->cfg.device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  flush_events(h);
+  if (h->arena) (void)hipFree(h->arena);
+  if (h->d_faults) (void)hipFree(h->d_faults);
+  if (h->d_scratch) (void)hipFree(h->d_scratch);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return 0;
+}
+
+extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload* wl, const paxisim_fault_process* fp,
+                              paxisim** out) {
+  if (!cfg || !wl || !out) return fail(PAXISIM_EINVAL, "null argument");
+  paxisim_fault_process nofp;
+  memset(&nofp, 0, sizeof nofp);
+  if (!fp) fp = &nofp;
+  uint32_t N = 0;
+  int rc0 = check_config(cfg, wl, fp, &N);
+  if (rc0) return rc0;
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (cfg->device < 0 || cfg->device >= ndev) return fail(PAXISIM_EDEVICE, "device %d not present (%d visible)", cfg->device, ndev);
+  HIPCHK(hipSetDevice(cfg->device));
+
+  paxisim* h = new (std::nothrow) paxisim();
+  if (!h) return fail(PAXISIM_ENOMEM, "oom");
+  h->cfg = *cfg;
+  h->wl = *wl;
+  h->fp = *fp;
+  h->S = cfg->steps_per_launch ? cfg->steps_per_launch : 32;
+  Params& P = h->P;
+  memset(&P, 0, sizeof P);
+  P.N = N;
+  P.Z = cfg->n_zones;
+  P.W = cfg->window;
+  P.M = cfg->mbox_cap;
+  P.D = cfg->max_delay + 2u;
+  P.NS = N + 1u;
+  P.WK = wl->outstanding;
+  P.max_requests = wl->max_requests;
+  P.clusters = cfg->clusters;
+  P.C = (cfg->clusters + LANES - 1) / LANES * LANES;
+  P.cluster_base = cfg->cluster_base;
+  P.seed = cfg->seed;
+  P.q1 = cfg->q1;
+  P.q2 = cfg->q2;
+  P.fz = cfg->fz;
+  P.thrifty = cfg->thrifty;
+  P.ephemeral = cfg->ephemeral_leader;
+  P.rwc = cfg->reply_when_commit;
+  P.max_delay = cfg->max_delay;
+  P.drop_ppm = fp->drop_ppm;
+  P.drop_len = fp->drop_len;
+  P.slow_ppm = fp->slow_ppm;
+  P.slow_len = fp->slow_len;
+  P.slow_min = fp->slow_min;
+  P.slow_max = fp->slow_max;
+  uint32_t r = 0;
+  for (uint32_t z = 0; z < P.Z; z++) {
+    P.npz[z] = cfg->npz[z];
+    P.zmask[z] = ((1u << cfg->npz[z]) - 1u) << r;
+    for (uint32_t k = 0; k < cfg->npz[z]; k++, r++) {
+      h->zone_of[r] = z + 1;
+      h->node_of[r] = k + 1;
+    }
+  }
+  for (uint32_t w = 0; w < PAXISIM_MAX_WORKERS; w++) P.target[w] = wl->target[w];
+
+  const size_t C = P.C, NC = (size_t)N * C;
+  // size the arena (rec last: it is the only region not zeroed)
+  size_t zero_bytes = 0, total = 0;
+  {
+    char* p = nullptr;
+    carve<uint32_t>(p, NC * 7);
+    carve<uint64_t>(p, NC);
+    carve<uint64_t>(p, C);
+    carve<uint32_t>(p, C);
+    carve<uint32_t>(p, NC * PMAX);
+    carve<uint32_t>(p, NC * FMAX);
+    carve<uint32_t>(p, NC * N * 3);
+    carve<uint32_t>(p, NC * CKR);
+    carve<uint64_t>(p, NC * CKR);
+    carve<uint32_t>(p, NC * NSTAT);
+    carve<uint32_t>(p, C * P.WK * 2);
+    carve<uint4>(p, NC * P.W);
+    carve<uint8_t>(p, (size_t)P.D * N * P.NS * C);
+    zero_bytes = (size_t)p;
+    carve<uint4>(p, (size_t)P.D * N * P.NS * P.M * C);
+    total = (size_t)p;
+  }
+  hipError_t e = hipMalloc(&h->arena, total);
+  if (e != hipSuccess) {
+    delete h;
+    return fail(PAXISIM_ENOMEM, "hipMalloc(%zu bytes) failed: %s", total, hipGetErrorString(e));
+  }
+  h->arena_bytes = total;
+  {
+    char* p = (char*)h->arena;
+    uint32_t* s7 = carve<uint32_t>(p, NC * 7);
+    P.ballot = s7;
+    P.slot = s7 + NC;
+    P.execute = s7 + 2 * NC;
+    P.meta = s7 + 3 * NC;
+    P.flags = s7 + 4 * NC;
+    P.npend = s7 + 5 * NC;
+    P.nfwd = s7 + 6 * NC;
+    P.digest = carve<uint64_t>(p, NC);
+    P.kc = carve<uint64_t>(p, C);
+    P.poison = carve<uint32_t>(p, C);
+    P.pend = carve<uint32_t>(p, NC * PMAX);
+    P.fwd = carve<uint32_t>(p, NC * FMAX);
+    uint32_t* f3 = carve<uint32_t>(p, NC * N * 3);
+    P.drop_until = f3;
+    P.slow_until = f3 + NC * N;
+    P.slow_delay = f3 + 2 * NC * N;
+    P.ck_e = carve<uint32_t>(p, NC * CKR);
+    P.ck_d = carve<uint64_t>(p, NC * CKR);
+    P.stats = carve<uint32_t>(p, NC * NSTAT);
+    uint32_t* wk = carve<uint32_t>(p, C * P.WK * 2);
+    P.wk_cur = wk;
+    P.wk_issued = wk + C * P.WK;
+    P.log = carve<uint4>(p, NC * P.W);
+    P.cnt = carve<uint8_t>(p, (size_t)P.D * N * P.NS * C);
+    P.rec = carve<uint4>(p, (size_t)P.D * N * P.NS * P.M * C);
+  }
+  int rc1 = 0;
+  if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipMalloc(&h->d_scratch, sizeof(uint64_t) * 64)) != hipSuccess ||
+      (e = hipMalloc(&h->d_faults, sizeof(paxisim_fault) * PAXISIM_MAX_FAULTS)) != hipSuccess ||
+      (e = hipMemsetAsync(h->arena, 0, zero_bytes, h->stream)) != hipSuccess)
+    rc1 = fail(PAXISIM_EDEVICE, "device setup failed: %s", hipGetErrorString(e));
+  if (!rc1) {
+    P.faults = h->d_faults;
+    init_kernel<<<(unsigned)((C + 255) / 256), 256, 0, h->stream>>>(P);
+    if ((e = hipGetLastError()) != hipSuccess || (e = hipStreamSynchronize(h->stream)) != hipSuccess)
+      rc1 = fail(PAXISIM_EDEVICE, "init kernel failed: %s", hipGetErrorString(e));
+  }
+  if (rc1) {
+    paxisim_destroy(h);
+    return rc1;
+  }
+  *out = h;
+  return 0;
+}
+
+extern "C" int paxisim_fault_add(paxisim* h, const paxisim_fault* f) {
+  if (!h || !f) return fail(PAXISIM_EINVAL, "null argument");
+  if (h->faults.size() == PAXISIM_MAX_FAULTS) return fail(PAXISIM_EINVAL, "fault table full");
+  if (f->kind > PAXISIM_FAULT_CRASH || f->src >= h->P.N || (f->dst != PAXISIM_ALL_DST && f->dst >= h->P.N))
+    return fail(PAXISIM_EINVAL, "bad fault");
+  if (f->kind == PAXISIM_FAULT_SLOW && f->param > h->cfg.max_delay)
+    return fail(PAXISIM_EINVAL, "slow delay exceeds max_delay");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  h->faults.push_back(*f);
+  HIPCHK(hipMemcpyAsync(h->d_faults, h->faults.data(), h->faults.size() * sizeof(paxisim_fault),
+                        hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->P.nfaults = (uint32_t)h->faults.size();
+  return 0;
+}
+
+template <int NT>
+static void launch_steps(paxisim* h, uint32_t t0, uint32_t n) {
+  const Params& P = h->P;
+  const unsigned grid = (unsigned)(P.C / LANES);
+  paxos_steps<NT><<<grid, P.N * LANES, 0, h->stream>>>(P, t0, n);
+}
+
+extern "C" int paxisim_step(paxisim* h, uint32_t nsteps) {
+  if (!h) return fail(PAXISIM_EINVAL, "null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  while (nsteps > 0) {
+    const uint32_t n = nsteps < h->S ? nsteps : h->S;
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(hipEventRecord(a, h->stream));
+    switch (h->P.N) {
+      case 3: launch_steps<3>(h, h->t, n); break;
+      case 5: launch_steps<5>(h, h->t, n); break;
+      case 9: launch_steps<9>(h, h->t, n); break;
+      default: launch_steps<0>(h, h->t, n); break;
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(b, h->stream));
+    h->evs.emplace_back(a, b);
+    h->launches++;
+    h->t += n;
+    nsteps -= n;
+    if (h->evs.size() >= 256) {
+      int rc = flush_events(h);
+      if (rc) return rc;
+    }
+  }
+  return 0;
+}
+
+extern "C" int paxisim_sync(paxisim* h) {
+  if (!h) return fail(PAXISIM_EINVAL, "null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int paxisim_kernel_time(paxisim* h, double* ms, uint64_t* launches, int reset) {
+  if (!h) return fail(PAXISIM_EINVAL, "null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  int rc = flush_events(h);
+  if (rc) return rc;
+  if (ms) *ms = h->kernel_ms;
+  if (launches) *launches = h->launches;
+  if (reset) {
+    h->kernel_ms = 0;
+    h->launches = 0;
+  }
+  return 0;
+}
+
+extern "C" int paxisim_stats_get(paxisim* h, paxisim_stats* out) {
+  if (!h || !out) return fail(PAXISIM_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  uint64_t red[NRED];
+  HIPCHK(hipMemsetAsync(h->d_scratch, 0, sizeof(uint64_t) * NRED, h->stream));
+  stats_kernel<<<(unsigned)(h->P.C / 256 + 1), 256, 0, h->stream>>>(h->P, h->d_scratch);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(red, h->d_scratch, sizeof red, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  memset(out, 0, sizeof *out);
+  out->steps = h->t;
+  out->clusters = h->cfg.clusters;
+  for (int k = 0; k < PAXISIM_NMSG; k++) {
+    out->delivered[k] = red[ST_DELIV0 + k];
+    out->delivered_total += red[ST_DELIV0 + k];
+  }
+  out->client_requests = red[ST_CLIENT];
+  out->sent = red[ST_SENT];
+  out->dropped = red[ST_DROPPED];
+  out->discarded = red[ST_DISCARDED];
+  out->commits = red[ST_COMMITS];
+  out->replies = red[ST_REPLIES];
+  for (int b = 0; b < 8; b++) out->flagged[b] = red[NSTAT + b];
+  return 0;
+}
+
+extern "C" int paxisim_read_state(paxisim* h, uint64_t lo, uint64_t n, paxisim_replica_state* out) {
+  if (!h || !out) return fail(PAXISIM_EINVAL, "null argument");
+  if (lo + n > h->cfg.clusters || lo + n < lo) return fail(PAXISIM_ERANGE, "cluster range");
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const size_t cnt = (size_t)n * h->P.N;
+  paxisim_replica_state* d = nullptr;
+  HIPCHK(hipMalloc(&d, cnt * sizeof(paxisim_replica_state)));
+  gather_kernel<<<(unsigned)((cnt + 255) / 256), 256, 0, h->stream>>>(h->P, lo, n, d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d, cnt * sizeof(paxisim_replica_state), hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(PAXISIM_EDEVICE, "read_state: %s", hipGetErrorString(e));
+  for (size_t i = 0; i < cnt; i++) {       // expand to the 64-bit Ballot of ballot.go:15-17
+    const uint32_t b = (uint32_t)out[i].ballot;
+    if (b) {
+      const uint32_t id = b & 15u;
+      out[i].ballot = ((uint64_t)(b >> 4) << 32) | ((uint64_t)h->zone_of[id] << 16) | h->node_of[id];
+    }
+  }
+  return 0;
+}
+
+extern "C" int paxisim_check(paxisim* h, uint64_t* violations) {
+  if (!h || !violations) return fail(PAXISIM_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  HIPCHK(hipMemsetAsync(h->d_scratch, 0, sizeof(uint64_t), h->stream));
+  check_kernel<<<(unsigned)(h->P.C / 256 + 1), 256, 0, h->stream>>>(h->P, h->d_scratch);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(violations, h->d_scratch, sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int paxisim_device_bytes(paxisim* h, uint64_t* bytes) {
+  if (!h || !bytes) return fail(PAXISIM_EINVAL, "null argument");
+  *bytes = h->arena_bytes;
+  return 0;
+}

@@ -1,0 +1,121 @@
+"""Host-side mirror of the reference's simulation entry point over the HIP C-ABI.
+
+`Simulation` plays the role of `server -sim` (server/server.go:87-101) for a
+whole batch of clusters: it takes a paxi.Config-like description (zones and
+nodes per zone, quorum options, config.go:14-35), a benchmark workload
+(benchmark.go:21-48) and fault injection (socket.go:163-199), and advances all
+clusters on one GPU through libpaxisim.so.  There is no CPU fallback: if the
+HIP library or the device is missing, construction raises.
+"""
+import ctypes as C
+import os
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpaxisim.so")
+_lib = None
+
+
+class PaxisimError(RuntimeError):
+    pass
+
+
+def load_library():
+    """Load the in-tree HIP library; raise if it is absent (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PaxisimError(f"HIP library not built: {LIB_PATH} (run `python -c 'import __graft_entry__ as g; g.build()'`)")
+    L = C.CDLL(LIB_PATH)
+    abi.declare(L, "paxisim")
+    L.paxisim_abi_version.restype = C.c_int
+    L.paxisim_step.restype = C.c_int
+    L.paxisim_step.argtypes = [C.c_void_p, C.c_uint32]
+    L.paxisim_sync.restype = C.c_int
+    L.paxisim_sync.argtypes = [C.c_void_p]
+    L.paxisim_kernel_time.restype = C.c_int
+    L.paxisim_kernel_time.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.c_int]
+    L.paxisim_device_bytes.restype = C.c_int
+    L.paxisim_device_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+    if L.paxisim_abi_version() != abi.ABI_VERSION:
+        raise PaxisimError("ABI version mismatch between paxi_amd/abi.py and libpaxisim.so")
+    _lib = L
+    return L
+
+
+EXPORTED = ["paxisim_abi_version", "paxisim_last_error", "paxisim_create", "paxisim_destroy",
+            "paxisim_fault_add", "paxisim_step", "paxisim_sync", "paxisim_stats_get",
+            "paxisim_read_state", "paxisim_check", "paxisim_kernel_time", "paxisim_device_bytes"]
+
+
+def _check(rc):
+    if rc != 0:
+        raise PaxisimError(f"paxisim error {rc}: {load_library().paxisim_last_error().decode()}")
+
+
+class Simulation:
+    """A batch of independent N-replica clusters on one GPU (one handle)."""
+
+    def __init__(self, cfg, wl, fp=None, faults=()):
+        L = load_library()
+        self.cfg, self.wl, self.fp = cfg, wl, fp
+        self.N = abi.n_replicas(cfg)
+        self.h = C.c_void_p()
+        _check(L.paxisim_create(C.byref(cfg), C.byref(wl), C.byref(fp) if fp else None, C.byref(self.h)))
+        for f in faults:
+            self.fault(f)
+
+    # socket.go Drop/Slow/Flaky/Crash, scripted
+    def fault(self, f):
+        _check(load_library().paxisim_fault_add(self.h, C.byref(f)))
+
+    def step(self, n):
+        _check(load_library().paxisim_step(self.h, n))
+
+    def sync(self):
+        _check(load_library().paxisim_sync(self.h))
+
+    def stats(self):
+        s = abi.Stats()
+        _check(load_library().paxisim_stats_get(self.h, C.byref(s)))
+        return s
+
+    def read_state(self, lo=0, n=None):
+        n = self.cfg.clusters - lo if n is None else n
+        arr = (abi.ReplicaState * (n * self.N))()
+        _check(load_library().paxisim_read_state(self.h, lo, n, arr))
+        return arr
+
+    def check(self):
+        v = C.c_uint64()
+        _check(load_library().paxisim_check(self.h, C.byref(v)))
+        return v.value
+
+    def kernel_time(self, reset=False):
+        ms, n = C.c_double(), C.c_uint64()
+        _check(load_library().paxisim_kernel_time(self.h, C.byref(ms), C.byref(n), int(reset)))
+        return ms.value, n.value
+
+    def device_bytes(self):
+        b = C.c_uint64()
+        _check(load_library().paxisim_device_bytes(self.h, C.byref(b)))
+        return b.value
+
+    def close(self):
+        if self.h:
+            load_library().paxisim_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,116 @@
+"""Test-side loader for the CPU oracle (oracle/liboracle_paxisim.so).
+
+The oracle is test infrastructure: only tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg load it, and only as the checker.
+"""
+import ctypes as C
+import os
+
+from paxi_amd import abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle_paxisim.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            raise RuntimeError(f"oracle not built: run `make -C oracle` ({ORACLE_SO})")
+        L = C.CDLL(ORACLE_SO)
+        abi.declare(L, "oracle")
+        L.oracle_step.restype = C.c_int
+        L.oracle_step.argtypes = [C.c_void_p, C.c_uint32, C.c_int]
+        L.oracle_exec_log.restype = C.c_int
+        L.oracle_exec_log.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.POINTER(C.c_uint32),
+                                      C.c_uint32, C.POINTER(C.c_uint32)]
+        L.oracle_new_ballot.restype = C.c_uint64
+        L.oracle_new_ballot.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
+        L.oracle_ballot_next.restype = C.c_uint64
+        L.oracle_ballot_next.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32]
+        L.oracle_quorum.restype = C.c_int
+        L.oracle_quorum.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.c_uint32]
+        L.oracle_linearizable.restype = C.c_int
+        L.oracle_linearizable.argtypes = [C.POINTER(C.c_int64), C.c_int]
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError(f"oracle error {rc}: {lib().oracle_last_error().decode()}")
+
+
+class OracleSim:
+    """Same surface as paxi_amd.sim.Simulation, backed by the CPU restatement."""
+
+    def __init__(self, cfg, wl, fp=None, faults=()):
+        self.cfg, self.wl = cfg, wl
+        self.N = abi.n_replicas(cfg)
+        self.h = C.c_void_p()
+        _check(lib().oracle_create(C.byref(cfg), C.byref(wl), C.byref(fp) if fp else None, C.byref(self.h)))
+        for f in faults:
+            _check(lib().oracle_fault_add(self.h, C.byref(f)))
+
+    def step(self, n, threads=1):
+        _check(lib().oracle_step(self.h, n, threads))
+
+    def stats(self):
+        s = abi.Stats()
+        _check(lib().oracle_stats_get(self.h, C.byref(s)))
+        return s
+
+    def read_state(self, lo=0, n=None):
+        n = self.cfg.clusters - lo if n is None else n
+        arr = (abi.ReplicaState * (n * self.N))()
+        _check(lib().oracle_read_state(self.h, lo, n, arr))
+        return arr
+
+    def check(self):
+        v = C.c_uint64()
+        _check(lib().oracle_check(self.h, C.byref(v)))
+        return v.value
+
+    def exec_log(self, cluster, replica):
+        n = C.c_uint32()
+        _check(lib().oracle_exec_log(self.h, cluster, replica, None, 0, C.byref(n)))
+        buf = (C.c_uint32 * max(1, n.value))()
+        _check(lib().oracle_exec_log(self.h, cluster, replica, buf, n.value, C.byref(n)))
+        return list(buf[: n.value])
+
+    def close(self):
+        if self.h:
+            lib().oracle_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def new_ballot(n, zone, node):
+    return lib().oracle_new_ballot(n, zone, node)
+
+
+def ballot_next(b, zone, node):
+    return lib().oracle_ballot_next(b, zone, node)
+
+
+def quorum(kind, npz, mask, fz=0):
+    arr = (C.c_uint32 * len(npz))(*npz)
+    return bool(lib().oracle_quorum(kind, fz, len(npz), arr, mask))
+
+
+def linearizable(ops):
+    """ops: list of (input, output, start, end) with None for nil (operation.go)."""
+    flat = []
+    for i, o, s, e in ops:
+        flat += [0 if i is None else 1, 0 if i is None else i, 0 if o is None else 1, 0 if o is None else o, s, e]
+    arr = (C.c_int64 * len(flat))(*flat)
+    n = lib().oracle_linearizable(arr, len(ops))
+    if n < 0:
+        raise RuntimeError("linearizable failed")
+    return n
