@@ -99,7 +99,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--clusters", type=int, default=1 << 20, help="clusters per GPU")
     ap.add_argument("--sim-steps", type=int, default=50, help="virtual steps per bench step (per launch)")
-    ap.add_argument("--window", type=int, default=32)
+    ap.add_argument("--window", type=int, default=16)
     ap.add_argument("--mbox", type=int, default=16)
     ap.add_argument("--cpu-clusters", type=int, default=16384)
     ap.add_argument("--cpu-steps", type=int, default=1600)

@@ -37,17 +37,27 @@ static inline uint64_t mix64(uint64_t z) {
   z ^= z >> 31;
   return z;
 }
-static inline uint64_t cluster_key(uint64_t seed, uint64_t gid) {
-  return mix64(seed ^ mix64(gid + 0x9E3779B97F4A7C15ULL));
+static inline uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x85ebca6bu;
+  h ^= h >> 13; h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
 }
-static inline uint64_t draw(uint64_t kc, uint32_t t, uint32_t tag) {
-  return mix64(kc ^ mix64(((uint64_t)t << 32) | tag));
+/* per-cluster 32-bit key, derived once from the 64-bit seed and global id */
+static inline uint32_t cluster_key(uint64_t seed, uint64_t gid) {
+  return (uint32_t)mix64(seed ^ mix64(gid + 0x9E3779B97F4A7C15ULL));
 }
+/* per-(cluster, step) stream key; every draw of that step hashes a tag into it */
+static inline uint32_t step_key(uint32_t kc, uint32_t t) { return fmix32(kc ^ (t * 0x9E3779B1u)); }
+static inline uint32_t draw(uint32_t hs, uint32_t tag) { return fmix32(hs ^ tag); }
 #define TAG(p, a, b) (((uint32_t)(p) << 28) | ((uint32_t)(a) << 20) | (uint32_t)(b))
 enum { PUR_ORDER = 1, PUR_LINK = 2, PUR_SLOWD = 3, PUR_FLAKY = 4, PUR_WL = 5 };
+/* P(x32 hits) = ppm / 1e6 */
 static inline int ppm_hit(uint32_t x, uint32_t ppm) {
   return (uint32_t)(((uint64_t)x * 1000000ULL) >> 32) < ppm;
 }
+/* 16-bit variant: (x16 * 1e6) >> 16 == (x16 * 15625) >> 10 exactly */
+static inline int ppm_hit16(uint32_t x16, uint32_t ppm) { return ((x16 * 15625u) >> 10) < ppm; }
 
 /* ------------------------------------------------------------------------ */
 /* Ballot / ID (ballot.go:15-52, id.go:14-69).  In-simulation a ballot is      */
@@ -159,7 +169,8 @@ typedef struct replica {
 } replica_t;
 
 typedef struct cluster {
-  uint64_t gid, kc;
+  uint64_t gid;
+  uint32_t kc;
   uint32_t poison_step;            /* first step at which a replica panicked */
   uint32_t wk_cur[PAXISIM_MAX_WORKERS], wk_issued[PAXISIM_MAX_WORKERS];
   replica_t rep[PAXISIM_MAX_N];
@@ -186,7 +197,7 @@ typedef struct ctx {
   const struct oracle_sim* s;
   cluster_t* c;
   replica_t* p;
-  uint32_t r, t;
+  uint32_t r, t, hs;
   int stop;                        /* replica panicked in this step */
 } ctx_t;
 
@@ -235,7 +246,7 @@ static void sock_send(ctx_t* x, uint32_t to, const rec_t* recs, uint32_t nrec) {
   if (x->t < p->drop_until[to] ||
       scripted(s, PAXISIM_FAULT_DROP, x->c->gid, x->r, to, x->t, NULL)) { p->dropped++; return; } /* 73 */
   if (scripted(s, PAXISIM_FAULT_FLAKY, x->c->gid, x->r, to, x->t, &flaky) && flaky > 0) {         /* 77-81 */
-    uint32_t u = (uint32_t)(draw(x->c->kc, x->t, TAG(PUR_FLAKY, x->r, seq)) >> 32);
+    uint32_t u = draw(x->hs, TAG(PUR_FLAKY, x->r, seq));
     if (ppm_hit(u, flaky)) { p->dropped++; return; }
   }
   if (x->t < p->slow_until[to]) delay = p->slow_delay[to];        /* 99-106 */
@@ -656,14 +667,14 @@ static void fault_process(ctx_t* x) {
   uint32_t d;
   if (fp->drop_ppm == 0 && fp->slow_ppm == 0) return;
   for (d = 0; d < s->N; d++) {
-    uint64_t u;
+    uint32_t u;
     if (d == x->r) continue;
-    u = draw(x->c->kc, x->t, TAG(PUR_LINK, x->r, d));
-    if (fp->drop_ppm && x->t >= p->drop_until[d] && ppm_hit((uint32_t)u, fp->drop_ppm))
+    u = draw(x->hs, TAG(PUR_LINK, x->r, d));
+    if (fp->drop_ppm && x->t >= p->drop_until[d] && ppm_hit16(u & 0xFFFFu, fp->drop_ppm))
       p->drop_until[d] = x->t + fp->drop_len;
-    if (fp->slow_ppm && x->t >= p->slow_until[d] && ppm_hit((uint32_t)(u >> 32), fp->slow_ppm)) {
+    if (fp->slow_ppm && x->t >= p->slow_until[d] && ppm_hit16(u >> 16, fp->slow_ppm)) {
       uint32_t span = fp->slow_max - fp->slow_min + 1u;
-      uint32_t v = (uint32_t)(draw(x->c->kc, x->t, TAG(PUR_SLOWD, x->r, d)) >> 32);
+      uint32_t v = draw(x->hs, TAG(PUR_SLOWD, x->r, d));
       p->slow_until[d] = x->t + fp->slow_len;
       p->slow_delay[d] = fp->slow_min + (uint32_t)(((uint64_t)v * span) >> 32);
     }
@@ -675,6 +686,7 @@ static void replica_step(const struct oracle_sim* s, cluster_t* c, uint32_t r, u
   uint32_t b = t % s->D, src, rem[PAXISIM_MAX_N + 1], pos[PAXISIM_MAX_N + 1], total = 0, i;
   int crash;
   x.s = s; x.c = c; x.p = &c->rep[r]; x.r = r; x.t = t; x.stop = 0;
+  x.hs = step_key(c->kc, t);
   x.p->send_seq = 0;
   fault_process(&x);
   crash = crashed(s, c, r, t);
@@ -693,8 +705,8 @@ static void replica_step(const struct oracle_sim* s, cluster_t* c, uint32_t r, u
     total += rem[src];
   }
   for (i = 0; total > 0 && !x.stop; i++) {
-    uint32_t u = (uint32_t)(draw(c->kc, t, TAG(PUR_ORDER, r, i)) >> 32);
-    uint32_t pick = (uint32_t)(((uint64_t)u * total) >> 32), len;
+    uint32_t u = draw(x.hs, TAG(PUR_ORDER, r, i >> 1));       /* two 16-bit picks per draw */
+    uint32_t pick = (((i & 1u) ? (u >> 16) : (u & 0xFFFFu)) * total) >> 16, len;
     rec_t* m;
     for (src = 0; pick >= rem[src]; src++) pick -= rem[src];
     m = mb_rec(s, c, b, r, src, pos[src]);

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <utility>
 #include <vector>
 
 #include "paxisim_dev.h"
@@ -59,17 +60,23 @@ extern "C" const char* paxisim_last_error(void) { return g_err; }
 __global__ void init_kernel(Params P) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= P.C) return;
+  const uint32_t blk = (uint32_t)(c / LANES), lane = (uint32_t)(c % LANES);
+  uint8_t* img = P.image + (size_t)blk * P.img.bytes;
   P.kc[c] = cluster_key(P.seed, P.cluster_base + c);
-  P.poison[c] = 0xFFFFFFFFu;
+  reinterpret_cast<uint32_t*>(img + P.img.off_poison)[lane] = 0xFFFFFFFFu;
   for (uint32_t r = 0; r < P.N; r++) P.slot[rc(P, r, c)] = 0xFFFFFFFFu;   // slot: -1 (paxos.go:45)
   if (c >= P.clusters) return;
+  uint8_t* cnt = img + P.img.off_cnt;
+  uint32_t* wcur = reinterpret_cast<uint32_t*>(img + P.img.off_wcur);
+  uint32_t* wiss = reinterpret_cast<uint32_t*>(img + P.img.off_wiss);
+  uint4* rec = P.rec + (size_t)blk * P.rec_per_block;
   for (uint32_t w = 0; w < P.WK; w++) {         // each worker's first request waits at step 0
-    const size_t bx = box(P, 0, P.target[w], P.N);
-    uint8_t* cp = cnt_at(P, bx, c);
-    *rec_at(P, bx, *cp, c) = make_uint4(PAXISIM_MSG_REQUEST, 0u, 0u, 1u + w);
-    *cp = (uint8_t)(*cp + 1u);
-    P.wk_cur[(size_t)w * P.C + c] = 1u + w;
-    P.wk_issued[(size_t)w * P.C + c] = 1u;
+    const uint32_t box = (0u * P.N + P.target[w]) * P.NS + P.N;
+    const uint32_t k = cnt[(box << 6) | lane];
+    rec[((box * P.M + k) << 6) | lane] = make_uint4(PAXISIM_MSG_REQUEST, 0u, 0u, 1u + w);
+    cnt[(box << 6) | lane] = (uint8_t)(k + 1u);
+    wcur[(w << 6) | lane] = 1u + w;
+    wiss[(w << 6) | lane] = 1u;
   }
 }
 
@@ -173,6 +180,10 @@ static int check_config(const paxisim_config* cfg, const paxisim_workload* wl, c
     if (wl->target[w] >= N) return fail(PAXISIM_EINVAL, "target[%u]", w);
   if (fp->slow_ppm && (fp->slow_min > fp->slow_max || fp->slow_max > cfg->max_delay))
     return fail(PAXISIM_EINVAL, "slow delay range exceeds max_delay");
+  const Image img = image_layout(N, cfg->window, wl->outstanding, cfg->max_delay + 2u);
+  if (img.bytes > LDS_MAX)
+    return fail(PAXISIM_EUNSUPP, "workgroup image %u B exceeds LDS (%u B): reduce window/max_delay/replicas",
+                img.bytes, LDS_MAX);
   *N_out = N;
   return 0;
 }
@@ -268,27 +279,38 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
   }
   for (uint32_t w = 0; w < PAXISIM_MAX_WORKERS; w++) P.target[w] = wl->target[w];
 
-  const size_t C = P.C, NC = (size_t)N * C;
+  const size_t C = P.C, NC = (size_t)N * C, blocks = C / LANES;
+  P.img = image_layout(N, P.W, P.WK, P.D);
+  P.rec_per_block = P.D * N * P.NS * P.M * LANES;
   // size the arena (rec last: it is the only region not zeroed)
   size_t zero_bytes = 0, total = 0;
+  auto layout = [&](char* p, bool assign) {
+    uint32_t* s7 = carve<uint32_t>(p, NC * 7);
+    uint64_t* dg = carve<uint64_t>(p, NC);
+    uint32_t* kc = carve<uint32_t>(p, C);
+    uint32_t* pend = carve<uint32_t>(p, NC * PMAX);
+    uint32_t* fwd = carve<uint32_t>(p, NC * FMAX);
+    uint32_t* links = carve<uint32_t>(p, NC * N * 2);
+    uint32_t* cke = carve<uint32_t>(p, NC * CKR);
+    uint64_t* ckd = carve<uint64_t>(p, NC * CKR);
+    uint32_t* st = carve<uint32_t>(p, NC * NSTAT);
+    uint32_t* reqx = carve<uint32_t>(p, NC * P.W);
+    uint8_t* image = carve<uint8_t>(p, blocks * P.img.bytes);
+    char* zend = p;
+    uint4* rec = carve<uint4>(p, blocks * P.rec_per_block);
+    if (assign) {
+      P.ballot = s7; P.slot = s7 + NC; P.execute = s7 + 2 * NC; P.meta = s7 + 3 * NC;
+      P.flags = s7 + 4 * NC; P.npend = s7 + 5 * NC; P.nfwd = s7 + 6 * NC;
+      P.digest = dg; P.kc = kc; P.pend = pend; P.fwd = fwd;
+      P.link_drop = links; P.link_slow = links + NC * N;
+      P.ck_e = cke; P.ck_d = ckd; P.stats = st; P.reqx = reqx; P.image = image; P.rec = rec;
+    }
+    return std::make_pair((size_t)zend, (size_t)p);
+  };
   {
-    char* p = nullptr;
-    carve<uint32_t>(p, NC * 7);
-    carve<uint64_t>(p, NC);
-    carve<uint64_t>(p, C);
-    carve<uint32_t>(p, C);
-    carve<uint32_t>(p, NC * PMAX);
-    carve<uint32_t>(p, NC * FMAX);
-    carve<uint32_t>(p, NC * N * 3);
-    carve<uint32_t>(p, NC * CKR);
-    carve<uint64_t>(p, NC * CKR);
-    carve<uint32_t>(p, NC * NSTAT);
-    carve<uint32_t>(p, C * P.WK * 2);
-    carve<uint4>(p, NC * P.W);
-    carve<uint8_t>(p, (size_t)P.D * N * P.NS * C);
-    zero_bytes = (size_t)p;
-    carve<uint4>(p, (size_t)P.D * N * P.NS * P.M * C);
-    total = (size_t)p;
+    auto sz = layout(nullptr, false);
+    zero_bytes = sz.first;
+    total = sz.second;
   }
   hipError_t e = hipMalloc(&h->arena, total);
   if (e != hipSuccess) {
@@ -296,35 +318,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     return fail(PAXISIM_ENOMEM, "hipMalloc(%zu bytes) failed: %s", total, hipGetErrorString(e));
   }
   h->arena_bytes = total;
-  {
-    char* p = (char*)h->arena;
-    uint32_t* s7 = carve<uint32_t>(p, NC * 7);
-    P.ballot = s7;
-    P.slot = s7 + NC;
-    P.execute = s7 + 2 * NC;
-    P.meta = s7 + 3 * NC;
-    P.flags = s7 + 4 * NC;
-    P.npend = s7 + 5 * NC;
-    P.nfwd = s7 + 6 * NC;
-    P.digest = carve<uint64_t>(p, NC);
-    P.kc = carve<uint64_t>(p, C);
-    P.poison = carve<uint32_t>(p, C);
-    P.pend = carve<uint32_t>(p, NC * PMAX);
-    P.fwd = carve<uint32_t>(p, NC * FMAX);
-    uint32_t* f3 = carve<uint32_t>(p, NC * N * 3);
-    P.drop_until = f3;
-    P.slow_until = f3 + NC * N;
-    P.slow_delay = f3 + 2 * NC * N;
-    P.ck_e = carve<uint32_t>(p, NC * CKR);
-    P.ck_d = carve<uint64_t>(p, NC * CKR);
-    P.stats = carve<uint32_t>(p, NC * NSTAT);
-    uint32_t* wk = carve<uint32_t>(p, C * P.WK * 2);
-    P.wk_cur = wk;
-    P.wk_issued = wk + C * P.WK;
-    P.log = carve<uint4>(p, NC * P.W);
-    P.cnt = carve<uint8_t>(p, (size_t)P.D * N * P.NS * C);
-    P.rec = carve<uint4>(p, (size_t)P.D * N * P.NS * P.M * C);
-  }
+  layout((char*)h->arena, true);
   int rc1 = 0;
   if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipMalloc(&h->d_scratch, sizeof(uint64_t) * 64)) != hipSuccess ||
@@ -362,14 +356,23 @@ extern "C" int paxisim_fault_add(paxisim* h, const paxisim_fault* f) {
 }
 
 template <int NT>
-static void launch_steps(paxisim* h, uint32_t t0, uint32_t n) {
+static hipError_t launch_steps(paxisim* h, uint32_t t0, uint32_t n) {
   const Params& P = h->P;
   const unsigned grid = (unsigned)(P.C / LANES);
-  paxos_steps<NT><<<grid, P.N * LANES, 0, h->stream>>>(P, t0, n);
+  static thread_local bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&paxos_steps<NT>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  paxos_steps<NT><<<grid, P.N * LANES, P.img.bytes, h->stream>>>(P, t0, n);
+  return hipGetLastError();
 }
 
 extern "C" int paxisim_step(paxisim* h, uint32_t nsteps) {
   if (!h) return fail(PAXISIM_EINVAL, "null handle");
+  if ((uint64_t)h->t + nsteps >= T_MAX) return fail(PAXISIM_EINVAL, "step counter would exceed 2^28");
   HIPCHK(hipSetDevice(h->cfg.device));
   while (nsteps > 0) {
     const uint32_t n = nsteps < h->S ? nsteps : h->S;
@@ -377,13 +380,14 @@ extern "C" int paxisim_step(paxisim* h, uint32_t nsteps) {
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
     HIPCHK(hipEventRecord(a, h->stream));
+    hipError_t le;
     switch (h->P.N) {
-      case 3: launch_steps<3>(h, h->t, n); break;
-      case 5: launch_steps<5>(h, h->t, n); break;
-      case 9: launch_steps<9>(h, h->t, n); break;
-      default: launch_steps<0>(h, h->t, n); break;
+      case 3: le = launch_steps<3>(h, h->t, n); break;
+      case 5: le = launch_steps<5>(h, h->t, n); break;
+      case 9: le = launch_steps<9>(h, h->t, n); break;
+      default: le = launch_steps<0>(h, h->t, n); break;
     }
-    HIPCHK(hipGetLastError());
+    if (le != hipSuccess) return fail(PAXISIM_EDEVICE, "step launch: %s", hipGetErrorString(le));
     HIPCHK(hipEventRecord(b, h->stream));
     h->evs.emplace_back(a, b);
     h->launches++;

@@ -1,12 +1,16 @@
 // paxisim_dev.h — device-side layout, PRNG and shared helpers of the HIP path.
 //
 // Execution model: one workgroup = N waves x 64 lanes.  Wave r
-// plays replica r, lane l plays cluster (64*blockIdx.x + l).  All state is
-// structure-of-arrays with the cluster index fastest, so a wave's access to a
-// field is one contiguous 256-byte (u32) run.  A workgroup owns its 64
-// clusters for the whole launch and advances them S steps, with one
-// __syncthreads() per step: messages sent in step t become visible to their
-// receivers in step t+1+delay through the bucketed mailboxes.
+// plays replica r, lane l plays cluster 64*blockIdx.x + l, so all replicas of
+// a cluster live in one workgroup and exchange messages through memory the
+// workgroup owns.  A workgroup advances its 64 clusters S steps per launch
+// with one __syncthreads() per step.
+//
+// Per launch the workgroup's hot state (log windows, mailbox counts, client
+// worker tables, poison flags) is copied from its HBM image into LDS and
+// back; message records stay in HBM in a block-contiguous region and are
+// prefetched one message ahead; replica scalars and socket fault state live
+// in registers.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -21,8 +25,14 @@ constexpr uint32_t CKI = 16;    // checkpoint interval (executed slots)
 constexpr uint32_t CKR = 8;     // checkpoints kept per replica
 constexpr uint32_t NO_ID = 0xFFu;
 constexpr uint32_t LANES = 64;
+constexpr uint32_t LDS_MAX = 160u * 1024u;
+constexpr uint32_t T_MAX = 1u << 28;   // slow_until is packed in 28 bits
 
-constexpr uint32_t E_EXISTS = 1u, E_COMMIT = 2u, E_QUORUM = 4u;
+// log entry, LDS form: {ballot, cmd | flags, ack mask}
+constexpr uint32_t CMD_MASK = 0x07FFFFFFu;
+constexpr uint32_t EF_EXISTS = 1u << 27, EF_COMMIT = 1u << 28, EF_QUORUM = 1u << 29;
+constexpr uint32_t EF_REQSELF = 1u << 30;   // request == (cmd, client): kept implicit
+constexpr uint32_t EF_REQEXT = 1u << 31;    // request in the HBM side table
 
 enum { PUR_ORDER = 1, PUR_LINK = 2, PUR_SLOWD = 3, PUR_FLAKY = 4 };
 
@@ -34,6 +44,25 @@ enum {
   NSTAT
 };
 
+// Byte layout of a workgroup's LDS image (identical in HBM, one per block).
+struct Image {
+  uint32_t off_bal, off_cmd, off_ack, off_wcur, off_wiss, off_poison, off_cnt, bytes;
+};
+
+__host__ __device__ inline Image image_layout(uint32_t N, uint32_t W, uint32_t WK, uint32_t D) {
+  Image m;
+  const uint32_t logb = N * W * LANES * 4u;
+  m.off_bal = 0;
+  m.off_cmd = m.off_bal + logb;
+  m.off_ack = m.off_cmd + logb;
+  m.off_wcur = m.off_ack + logb;
+  m.off_wiss = m.off_wcur + WK * LANES * 4u;
+  m.off_poison = m.off_wiss + WK * LANES * 4u;
+  m.off_cnt = m.off_poison + LANES * 4u;
+  m.bytes = (m.off_cnt + D * N * (N + 1u) * LANES + 15u) & ~15u;
+  return m;
+}
+
 struct Params {
   uint32_t N, Z, W, M, D, NS, WK, max_requests;
   uint64_t C;            // allocated cluster lanes (multiple of 64)
@@ -43,24 +72,22 @@ struct Params {
   uint32_t drop_ppm, drop_len, slow_ppm, slow_len, slow_min, slow_max;
   uint32_t npz[PAXISIM_MAX_ZONES], zmask[PAXISIM_MAX_ZONES];
   uint32_t target[PAXISIM_MAX_WORKERS];
+  Image img;
+  uint32_t rec_per_block;  // D*N*NS*M*64
   const paxisim_fault* faults;
   // replica scalars [r][C]
   uint32_t *ballot, *slot, *execute, *meta, *flags, *npend, *nfwd;
   uint64_t* digest;
-  // per-cluster [C]
-  uint64_t* kc;
-  uint32_t* poison;
-  // dynamic tables
+  uint32_t* kc;          // [C] per-cluster PRNG key
   uint32_t* pend;        // [PMAX][N][C]
   uint32_t* fwd;         // [FMAX][N][C]
-  uint32_t *drop_until, *slow_until, *slow_delay;  // [dst][N][C]
+  uint32_t *link_drop, *link_slow;  // [dst][N][C]: drop_until; slow_until | delay << 28
   uint32_t* ck_e;        // [CKR][N][C]
   uint64_t* ck_d;        // [CKR][N][C]
   uint32_t* stats;       // [NSTAT][N][C]
-  uint32_t *wk_cur, *wk_issued;  // [WK][C]
-  uint4* log;            // [N][C][W]
-  uint4* rec;            // [D][N dst][NS src][M][C]
-  uint8_t* cnt;          // [D][N dst][NS src][C]
+  uint32_t* reqx;        // [blk][N][W][64] request side table
+  uint8_t* image;        // [blk][img.bytes]
+  uint4* rec;            // [blk][D][dst][src][M][64]
 };
 
 // ---- PRNG ------------------------------------------------
@@ -70,27 +97,27 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z ^= z >> 31;
   return z;
 }
-__host__ __device__ __forceinline__ uint64_t cluster_key(uint64_t seed, uint64_t gid) {
-  return mix64(seed ^ mix64(gid + 0x9E3779B97F4A7C15ULL));
+__host__ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x85ebca6bu;
+  h ^= h >> 13; h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
 }
-__device__ __forceinline__ uint64_t draw(uint64_t kc, uint32_t t, uint32_t tag) {
-  return mix64(kc ^ mix64(((uint64_t)t << 32) | tag));
+__host__ __device__ __forceinline__ uint32_t cluster_key(uint64_t seed, uint64_t gid) {
+  return (uint32_t)mix64(seed ^ mix64(gid + 0x9E3779B97F4A7C15ULL));
 }
-__device__ __forceinline__ uint32_t tag(uint32_t p, uint32_t a, uint32_t b) {
-  return (p << 28) | (a << 20) | b;
-}
-__device__ __forceinline__ bool ppm_hit(uint32_t x, uint32_t ppm) {
-  return __umulhi(x, 1000000u) < ppm;
-}
+__device__ __forceinline__ uint32_t step_key(uint32_t kc, uint32_t t) { return fmix32(kc ^ (t * 0x9E3779B1u)); }
+__device__ __forceinline__ uint32_t draw(uint32_t hs, uint32_t tag) { return fmix32(hs ^ tag); }
+__device__ __forceinline__ uint32_t tag(uint32_t p, uint32_t a, uint32_t b) { return (p << 28) | (a << 20) | b; }
+__device__ __forceinline__ bool ppm_hit(uint32_t x, uint32_t ppm) { return __umulhi(x, 1000000u) < ppm; }
+__device__ __forceinline__ bool ppm_hit16(uint32_t x16, uint32_t ppm) { return ((x16 * 15625u) >> 10) < ppm; }
 
 // ---- ballots: (n << 4) | replica, 0 = none (ballot.go:12-52) -------------
 __device__ __forceinline__ uint32_t bal_id(uint32_t b) { return b ? (b & 15u) : NO_ID; }
-__device__ __forceinline__ uint32_t bal_next(uint32_t b, uint32_t self) {
-  return (((b >> 4) + 1u) << 4) | self;
-}
+__device__ __forceinline__ uint32_t bal_next(uint32_t b, uint32_t self) { return (((b >> 4) + 1u) << 4) | self; }
 
 // ---- requests: cid | origin << 27 (message.go:24-30) ---------------------
-__device__ __forceinline__ uint32_t req_cid(uint32_t q) { return q & 0x07FFFFFFu; }
+__device__ __forceinline__ uint32_t req_cid(uint32_t q) { return q & CMD_MASK; }
 __device__ __forceinline__ uint32_t req_origin(uint32_t q) { return q >> 27; }
 __device__ __forceinline__ uint32_t mkreq(uint32_t cid, uint32_t o) { return cid | (o << 27); }
 
@@ -101,6 +128,7 @@ __device__ __forceinline__ uint32_t hdr_n(uint32_t h) { return h >> 8; }
 // ---- quorum predicates on an ack mask (quorum.go:55-119) -----------------
 __device__ __forceinline__ bool quorum_ok(const Params& P, uint32_t kind, uint32_t mask) {
   const int size = __popc(mask);
+  if (kind == PAXISIM_Q_MAJORITY) return size > (int)(P.N / 2);
   uint32_t zones_any = 0, zones_maj = 0;
   bool col = false;
   for (uint32_t z = 0; z < P.Z; z++) {
@@ -110,7 +138,6 @@ __device__ __forceinline__ bool quorum_ok(const Params& P, uint32_t kind, uint32
     col |= c == P.npz[z];
   }
   switch (kind) {
-    case PAXISIM_Q_MAJORITY: return size > (int)(P.N / 2);
     case PAXISIM_Q_ALL: return size == (int)P.N;
     case PAXISIM_Q_FAST: return size >= (int)(P.N * 3 / 4);
     case PAXISIM_Q_GRID_ROW: return zones_any == P.Z;
@@ -142,18 +169,6 @@ __device__ __forceinline__ bool scripted(const Params& P, uint32_t kind, uint64_
 __device__ __forceinline__ size_t rc(const Params& P, uint32_t r, uint64_t c) { return (size_t)r * P.C + c; }
 __device__ __forceinline__ size_t krc(const Params& P, uint32_t k, uint32_t r, uint64_t c) {
   return ((size_t)k * P.N + r) * P.C + c;
-}
-__device__ __forceinline__ uint4* log_at(const Params& P, uint32_t r, uint64_t c, int32_t s) {
-  return &P.log[((size_t)r * P.C + c) * P.W + ((uint32_t)s & (P.W - 1u))];
-}
-__device__ __forceinline__ size_t box(const Params& P, uint32_t b, uint32_t dst, uint32_t src) {
-  return ((size_t)b * P.N + dst) * P.NS + src;
-}
-__device__ __forceinline__ uint4* rec_at(const Params& P, size_t bx, uint32_t k, uint64_t c) {
-  return &P.rec[(bx * P.M + k) * P.C + c];
-}
-__device__ __forceinline__ uint8_t* cnt_at(const Params& P, size_t bx, uint64_t c) {
-  return &P.cnt[bx * P.C + c];
 }
 
 }  // namespace pxs
