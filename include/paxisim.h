@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PAXISIM_ABI_VERSION 1
+#define PAXISIM_ABI_VERSION 2
 
 #define PAXISIM_MAX_N        16  /* replicas per cluster (ack masks are u16) */
 #define PAXISIM_MAX_ZONES    16
@@ -100,6 +100,7 @@ enum paxisim_msg {
 #define PAXISIM_F_UNFAITHFUL 0x10u /* bounded model may differ from unbounded Go from here */
 #define PAXISIM_F_POISON    0x20u  /* the Go reference would panic here; cluster frozen */
 #define PAXISIM_F_BALLOT_OVF 0x40u /* ballot counter beyond 2^27 */
+#define PAXISIM_F_HIST_OVF  0x80u  /* ABD op history full: later ops not recorded */
 
 /* ---- scripted faults (socket.go:163-199; http.go:137-162 admin hooks) ---- */
 enum paxisim_fault_kind {
@@ -127,6 +128,7 @@ typedef struct paxisim_config {
   uint32_t max_delay;         /* largest Slow delay in steps (<= PAXISIM_MAX_DELAY) */
   uint32_t keys;              /* keys per cluster (ABD/WPaxos instances) */
   uint32_t steps_per_launch;  /* HIP backend: steps fused per kernel launch (0 = auto) */
+  uint32_t history;           /* ABD: completed ops recorded per replica (0 = none) */
   int32_t  device;            /* HIP device ordinal */
   uint64_t clusters;          /* clusters held by this handle */
   uint64_t cluster_base;      /* global id of local cluster 0 (multi-GPU sharding) */
@@ -225,6 +227,17 @@ int  paxisim_check(paxisim* h, uint64_t* violations);
 /* Device time of the step kernels since the last reset (HIP events on the
  * launch stream), and the number of launches. */
 int  paxisim_kernel_time(paxisim* h, double* ms, uint64_t* launches, int reset);
+
+/* History.Linearizable (history.go:55-71, checker.go:69-104) over every
+ * (cluster, key) of the recorded ABD operations: anomalous reads, operations
+ * checked, and partitions skipped because they exceed the checker's 128-op
+ * graph (any pointer may be NULL). */
+int  paxisim_linearizable(paxisim* h, uint64_t* anomalies, uint64_t* ops, uint64_t* skipped);
+
+/* Completed ABD operations of one local cluster: 5 words per op {key,
+ * is_write, value, start step, end step}; replicas in index order, each in
+ * completion order (the canonical history order). */
+int  paxisim_history(paxisim* h, uint64_t cluster, uint32_t* buf, uint32_t cap_ops, uint32_t* n_out);
 
 /* Bytes of device memory held by the handle. */
 int  paxisim_device_bytes(paxisim* h, uint64_t* bytes);

@@ -139,8 +139,15 @@ typedef struct { uint32_t ballot, cmd, req, meta; } entry_t;
 
 #define PMAX 32
 #define FMAX 32
+#define KMAX 64  /* ABD keys per cluster */
 #define CKI 16   /* checkpoint every CKI executed slots */
 #define CKR 8    /* checkpoints kept per replica */
+
+/* ABD op table entry (abd/replica.go:17-24), ring indexed by coordinator cid */
+typedef struct { uint32_t tag, req, state, getmask, setmask, value, version, start; } abd_op_t;
+enum { ABD_FREE = 0, ABD_GET = 1, ABD_SET = 2, ABD_DONE = 3 };
+/* one completed client operation (operation.go:5-11), for History.Linearizable */
+typedef struct { uint32_t key, is_write, value, start, end; } hist_t;
 
 typedef struct replica {
   /* paxos.Paxos fields (paxos/paxos.go:21-38) */
@@ -166,6 +173,12 @@ typedef struct replica {
   /* exec log (KATs) */
   uint32_t* xlog;
   uint32_t nx, capx;
+  /* ABD (abd/replica.go:28-34): cid counter, versioned KV, op table */
+  uint32_t abd_cid;
+  uint32_t *kv_val, *kv_ver;
+  abd_op_t* ops;
+  hist_t* hist;                    /* completed ops coordinated here (cfg.history of them) */
+  uint32_t nh;
 } replica_t;
 
 typedef struct cluster {
@@ -190,6 +203,7 @@ struct oracle_sim {
   cluster_t* cl;
   uint32_t t;                      /* next step to simulate */
   int keep_xlog;
+  uint32_t OW;                     /* ABD op table size */
 };
 
 /* handler context: one replica of one cluster at one step */
@@ -658,6 +672,136 @@ static void paxos_dispatch(ctx_t* x, uint32_t src, const rec_t* m) {
 }
 
 /* ------------------------------------------------------------------------ */
+/* Workload: key and read/write of command cid (benchmark.go:202-275)        */
+/* ------------------------------------------------------------------------ */
+static inline uint32_t wl_hash(uint32_t kc, uint32_t cid) { return fmix32(fmix32(kc ^ 0x5BD1E995u) ^ cid); }
+static inline uint32_t wl_key(const struct oracle_sim* s, uint32_t kc, uint32_t cid) {
+  return wl_hash(kc, cid) % s->cfg.keys;
+}
+static inline int wl_write(const struct oracle_sim* s, uint32_t kc, uint32_t cid) {
+  return ppm_hit(fmix32(wl_hash(kc, cid) ^ 0x27D4EB2Fu), s->wl.write_ppm);
+}
+
+/* ------------------------------------------------------------------------ */
+/* ABD atomic storage (abd/replica.go)                                       */
+/* Record fields: hdr = type | key << 8, ballot = coordinator op id (CID),   */
+/* slot = version, cid = value (a write's value is its command id; 0 = nil). */
+/* ------------------------------------------------------------------------ */
+static void abd_send(ctx_t* x, uint32_t to, uint32_t type, uint32_t key, uint32_t opid, uint32_t ver, uint32_t val) {
+  rec_t m;
+  m.hdr = HDR(type, key); m.ballot = opid; m.slot = ver; m.cid = val;
+  sock_send(x, to, &m, 1);
+}
+static void abd_broadcast(ctx_t* x, uint32_t type, uint32_t key, uint32_t opid, uint32_t ver, uint32_t val) {
+  uint32_t d;
+  for (d = 0; d < x->s->N; d++)
+    if (d != x->r) abd_send(x, d, type, key, opid, ver, val);
+}
+static inline int majority(const ctx_t* x, uint32_t mask) { return popc(mask) > (int)(x->s->N / 2); } /* quorum.go:60-62 */
+
+/* database.Put (db.go:123-134): only a non-nil value is written */
+static inline void abd_put(replica_t* p, uint32_t key, uint32_t val) { if (val) p->kv_val[key] = val; }
+
+static void abd_handle_request(ctx_t* x, uint32_t cid) {                    /* abd/replica.go:50-71 */
+  replica_t* p = x->p;
+  const uint32_t k = wl_key(x->s, x->c->kc, cid);
+  abd_op_t* e;
+  p->abd_cid++;
+  e = &p->ops[p->abd_cid & (x->s->OW - 1u)];
+  if (e->state == ABD_GET || e->state == ABD_SET)
+    raise_flag(x, PAXISIM_F_PEND_OVF | PAXISIM_F_UNFAITHFUL);               /* evicting a live op */
+  e->tag = p->abd_cid;
+  e->req = cid;
+  e->state = ABD_GET;
+  e->getmask = 1u << x->r;
+  e->setmask = 0;
+  e->value = p->kv_val[k];
+  e->version = p->kv_ver[k];
+  e->start = x->t;
+  abd_broadcast(x, PAXISIM_MSG_GET, k, p->abd_cid, 0, 0);
+}
+
+static void abd_handle_get(ctx_t* x, uint32_t src, uint32_t key, uint32_t opid) { /* abd/replica.go:73-82 */
+  abd_send(x, src, PAXISIM_MSG_GETREPLY, key, opid, x->p->kv_ver[key], x->p->kv_val[key]);
+}
+
+static void abd_handle_set(ctx_t* x, uint32_t src, uint32_t key, uint32_t opid, uint32_t ver, uint32_t val) { /* 84-95 */
+  replica_t* p = x->p;
+  if (ver > p->kv_ver[key]) {
+    abd_put(p, key, val);
+    p->kv_ver[key] = ver;
+  }
+  abd_send(x, src, PAXISIM_MSG_SETREPLY, key, opid, 0, 0);
+}
+
+static abd_op_t* abd_op(ctx_t* x, uint32_t opid) {
+  abd_op_t* e = &x->p->ops[opid & (x->s->OW - 1u)];
+  return e->tag == opid ? e : NULL;   /* a retired op: Go's entry is Done, or was flagged when evicted */
+}
+
+static void abd_handle_getreply(ctx_t* x, uint32_t src, uint32_t key, uint32_t opid, uint32_t ver, uint32_t val) { /* 97-136 */
+  replica_t* p = x->p;
+  abd_op_t* e = abd_op(x, opid);
+  if (!e || e->state != ABD_GET) return;
+  if (ver > e->version) {
+    e->value = val;
+    e->version = ver;
+    abd_put(p, key, val);
+    p->kv_ver[key] = ver;
+  }
+  e->getmask |= 1u << src;
+  if (majority(x, e->getmask)) {
+    e->state = ABD_SET;
+    e->setmask |= 1u << x->r;
+    if (!wl_write(x->s, x->c->kc, e->req)) {
+      abd_broadcast(x, PAXISIM_MSG_SET, key, opid, e->version, e->value);
+    } else {
+      e->value = e->req;                                                    /* the write's value */
+      e->version++;
+      abd_put(p, key, e->value);
+      p->kv_ver[key] = e->version;
+      abd_broadcast(x, PAXISIM_MSG_SET, key, opid, e->version, e->value);
+    }
+  }
+}
+
+static void abd_handle_setreply(ctx_t* x, uint32_t src, uint32_t key, uint32_t opid) { /* 138-157 */
+  cluster_t* c = x->c;
+  abd_op_t* e = abd_op(x, opid);
+  if (!e || e->state != ABD_SET) return;
+  e->setmask |= 1u << src;
+  if (majority(x, e->setmask)) {
+    int w = wl_write(x->s, c->kc, e->req);
+    replica_t* p = x->p;
+    e->state = ABD_DONE;
+    p->commits++;
+    if (p->nh < x->s->cfg.history) {                 /* History.AddOperation (history.go:44-52) */
+      hist_t* h = &p->hist[p->nh++];
+      h->key = key;
+      h->is_write = (uint32_t)w;
+      h->value = e->value;
+      h->start = e->start;
+      h->end = x->t;
+    } else if (x->s->cfg.history) {
+      raise_flag(x, PAXISIM_F_HIST_OVF);
+    }
+    client_reply(x, e->req);
+  }
+}
+
+static void abd_dispatch(ctx_t* x, uint32_t src, const rec_t* m) {
+  const uint32_t key = HDR_N(m->hdr);
+  switch (HDR_TYPE(m->hdr)) {
+    case PAXISIM_MSG_REQUEST: abd_handle_request(x, m->cid); break;
+    case PAXISIM_MSG_GET: abd_handle_get(x, src, key, m->ballot); break;
+    case PAXISIM_MSG_GETREPLY: abd_handle_getreply(x, src, key, m->ballot, m->slot, m->cid); break;
+    case PAXISIM_MSG_SET: abd_handle_set(x, src, key, m->ballot, m->slot, m->cid); break;
+    case PAXISIM_MSG_SETREPLY: abd_handle_setreply(x, src, key, m->ballot); break;
+    default: break;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
 /* One replica, one step                                    */
 /* ------------------------------------------------------------------------ */
 static void fault_process(ctx_t* x) {
@@ -716,7 +860,8 @@ static void replica_step(const struct oracle_sim* s, cluster_t* c, uint32_t r, u
     total -= len;
     if (src == s->N) x.p->client_requests++;
     else x.p->delivered[HDR_TYPE(m->hdr)]++;
-    paxos_dispatch(&x, src, m);
+    if (s->cfg.protocol == PAXISIM_ABD) abd_dispatch(&x, src, m);
+    else paxos_dispatch(&x, src, m);
   }
   for (src = 0; src < s->NS; src++) *mb_cnt(s, c, b, r, src) = 0;
   if (x.stop && c->poison_step > t) c->poison_step = t;
@@ -734,7 +879,9 @@ static void cluster_step(const struct oracle_sim* s, cluster_t* c, uint32_t t) {
 static int check_config(const paxisim_config* cfg, const paxisim_workload* wl,
                         const paxisim_fault_process* fp, uint32_t* N_out) {
   uint32_t z, N = 0, w;
-  if (cfg->protocol != PAXISIM_PAXOS) return fail(PAXISIM_EUNSUPP, "protocol %u not built", cfg->protocol);
+  if (cfg->protocol != PAXISIM_PAXOS && cfg->protocol != PAXISIM_ABD)
+    return fail(PAXISIM_EUNSUPP, "protocol %u not built", cfg->protocol);
+  if (cfg->protocol == PAXISIM_ABD && (cfg->keys < 1 || cfg->keys > KMAX)) return fail(PAXISIM_EINVAL, "keys");
   if (cfg->n_zones < 1 || cfg->n_zones > PAXISIM_MAX_ZONES) return fail(PAXISIM_EINVAL, "n_zones");
   for (z = 0; z < cfg->n_zones; z++) {
     if (cfg->npz[z] < 1) return fail(PAXISIM_EINVAL, "npz[%u] must be >= 1", z);
@@ -757,6 +904,12 @@ static int check_config(const paxisim_config* cfg, const paxisim_workload* wl,
   return 0;
 }
 
+static uint32_t abd_ow(uint32_t outstanding) {  /* ABD op table: pow2 >= 2*outstanding, >= 4 */
+  uint32_t ow = 4;
+  while (ow < 2u * outstanding) ow <<= 1;
+  return ow;
+}
+
 static void cluster_init(struct oracle_sim* s, cluster_t* c, uint64_t gid, entry_t* logs) {
   uint32_t r, w;
   memset(c->rep, 0, sizeof c->rep);
@@ -766,6 +919,12 @@ static void cluster_init(struct oracle_sim* s, cluster_t* c, uint64_t gid, entry
   for (r = 0; r < s->N; r++) {
     c->rep[r].slot = -1;                                   /* paxos.go:45 */
     c->rep[r].log = logs + (size_t)r * s->W;
+    if (s->cfg.protocol == PAXISIM_ABD) {
+      c->rep[r].kv_val = (uint32_t*)calloc(2u * s->cfg.keys, sizeof(uint32_t));
+      c->rep[r].kv_ver = c->rep[r].kv_val + s->cfg.keys;
+      c->rep[r].ops = (abd_op_t*)calloc(s->OW, sizeof(abd_op_t));
+      c->rep[r].hist = (hist_t*)calloc(s->cfg.history ? s->cfg.history : 1, sizeof(hist_t));
+    }
   }
   memset(c->wk_cur, 0, sizeof c->wk_cur);
   memset(c->wk_issued, 0, sizeof c->wk_issued);
@@ -804,6 +963,7 @@ int oracle_create(const paxisim_config* cfg, const paxisim_workload* wl,
   }
   s->C = cfg->clusters;
   s->keep_xlog = cfg->clusters <= 16;
+  s->OW = abd_ow(wl->outstanding);
   s->cl = (cluster_t*)calloc(s->C, sizeof(cluster_t));
   if (!s->cl) { free(s); return fail(PAXISIM_ENOMEM, "oom clusters"); }
   for (i = 0; i < s->C; i++) {
@@ -825,7 +985,12 @@ int oracle_destroy(oracle_sim* s) {
   for (i = 0; i < s->C; i++) {
     cluster_t* c = &s->cl[i];
     if (c->rep[0].log) free(c->rep[0].log);
-    for (r = 0; r < s->N; r++) free(c->rep[r].xlog);
+    for (r = 0; r < s->N; r++) {
+      free(c->rep[r].xlog);
+      free(c->rep[r].kv_val);
+      free(c->rep[r].ops);
+      free(c->rep[r].hist);
+    }
     free(c->mbox);
     free(c->cnt);
   }
@@ -892,6 +1057,17 @@ static void fill_state(const struct oracle_sim* s, const cluster_t* c, uint32_t 
   o->p1_acks = p->p1mask;
   o->npending = p->npend;
   memcpy(o->delivered, p->delivered, sizeof o->delivered);
+  if (s->cfg.protocol == PAXISIM_ABD) {            /* ABD: op counter, Done ops, KV digest, live ops */
+    uint32_t k, live = 0;
+    uint64_t d = 0;
+    for (k = 0; k < s->cfg.keys; k++) d = mix64(d ^ (((uint64_t)p->kv_ver[k] << 32) | p->kv_val[k]));
+    for (k = 0; k < s->OW; k++) live += p->ops[k].state == ABD_GET || p->ops[k].state == ABD_SET;
+    o->ballot = 0;
+    o->slot = (int32_t)p->abd_cid;
+    o->execute = (int32_t)p->nh;
+    o->digest = d;
+    o->npending = live;
+  }
   o->client_requests = p->client_requests;
   o->sent = p->sent;
   o->dropped = p->dropped;
@@ -1094,4 +1270,64 @@ int oracle_linearizable(const int64_t* ops, int n) {
   }
   free(g.hin); free(g.present); free(g.order); free(g.adj); free(idx); free(color);
   return anomalies;
+}
+
+/* History.Linearizable (history.go:55-71): run the checker on every
+ * (cluster, key) partition of the completed-operation history. */
+int oracle_lin_check(oracle_sim* s, uint64_t* anomalies, uint64_t* ops) {
+  uint64_t i, a = 0, n = 0;
+  uint32_t k, j;
+  int64_t* buf = NULL;
+  size_t cap = 0;
+  if (!s || !anomalies) return fail(PAXISIM_EINVAL, "null argument");
+  for (i = 0; i < s->C; i++) {
+    const cluster_t* c = &s->cl[i];
+    for (k = 0; k < s->cfg.keys; k++) {
+      int m = 0, res;
+      uint32_t r, nall = 0;
+      for (r = 0; r < s->N; r++) nall += c->rep[r].nh;
+      for (j = 0, r = 0; r < s->N; r++)
+      for (j = 0; j < c->rep[r].nh; j++) {
+        const hist_t* h = &c->rep[r].hist[j];
+        if (h->key != k) continue;
+        if ((size_t)(m + 1) * 6 > cap) {
+          cap = cap ? 2 * cap : 6 * 256;
+          buf = (int64_t*)realloc(buf, cap * sizeof(int64_t));
+        }
+        buf[6 * m + 0] = h->is_write ? 1 : 0;
+        buf[6 * m + 1] = h->is_write ? h->value : 0;
+        buf[6 * m + 2] = h->is_write ? 0 : 1;
+        buf[6 * m + 3] = h->is_write ? 0 : h->value;
+        buf[6 * m + 4] = h->start;
+        buf[6 * m + 5] = h->end;
+        m++;
+      }
+      (void)nall;
+      n += (uint64_t)m;
+      if (m == 0) continue;
+      res = oracle_linearizable(buf, m);
+      if (res < 0) { free(buf); return fail(PAXISIM_ENOMEM, "checker failed"); }
+      a += (uint64_t)res;
+    }
+  }
+  free(buf);
+  *anomalies = a;
+  if (ops) *ops = n;
+  return 0;
+}
+
+/* Raw completed-operation history of one cluster: 5 words per op
+ * {key, is_write, value, start, end}. */
+int oracle_history(oracle_sim* s, uint64_t cl, uint32_t* buf, uint32_t cap_ops, uint32_t* n_out) {
+  const cluster_t* c;
+  uint32_t r, n = 0;
+  if (!s || !n_out || cl >= s->C) return fail(PAXISIM_EINVAL, "bad argument");
+  c = &s->cl[cl];
+  for (r = 0; r < s->N; r++) {
+    uint32_t j;
+    for (j = 0; j < c->rep[r].nh; j++, n++)
+      if (buf && n < cap_ops) memcpy(buf + 5 * (size_t)n, &c->rep[r].hist[j], sizeof(hist_t));
+  }
+  *n_out = n;
+  return 0;
 }

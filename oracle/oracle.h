@@ -34,6 +34,9 @@ int  oracle_check(oracle_sim* h, uint64_t* violations);
 /* Executed command ids of (cluster, replica), in slot order (KAT support). */
 int  oracle_exec_log(oracle_sim* h, uint64_t cluster, uint32_t replica,
                      uint32_t* buf, uint32_t cap, uint32_t* n_out);
+/* History.Linearizable over every (cluster, key) of the ABD op history. */
+int  oracle_lin_check(oracle_sim* h, uint64_t* anomalies, uint64_t* ops);
+int  oracle_history(oracle_sim* h, uint64_t cluster, uint32_t* buf, uint32_t cap_ops, uint32_t* n_out);
 const char* oracle_last_error(void);
 
 /* Reference KAT helpers (ballot.go / quorum.go / checker.go restated). */

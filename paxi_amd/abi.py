@@ -6,7 +6,7 @@ structs, so the two speak exactly the same ABI.
 """
 import ctypes as C
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_N = 16
 MAX_ZONES = 16
 MAX_WORKERS = 32
@@ -36,8 +36,8 @@ MSG_NAMES = {MSG_REQUEST: "Request", MSG_REPLY: "Reply", MSG_P1A: "P1a", MSG_P1B
              MSG_LEADERCHG: "LeaderChange"}
 
 # flags
-F_WOVF, F_GHOST, F_MBOX_OVF, F_PEND_OVF, F_UNFAITHFUL, F_POISON, F_BALLOT_OVF = (
-    0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40)
+F_WOVF, F_GHOST, F_MBOX_OVF, F_PEND_OVF, F_UNFAITHFUL, F_POISON, F_BALLOT_OVF, F_HIST_OVF = (
+    0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80)
 
 # scripted faults (socket.go:163-199)
 FAULT_DROP, FAULT_SLOW, FAULT_FLAKY, FAULT_CRASH = 0, 1, 2, 3
@@ -60,6 +60,7 @@ class Config(C.Structure):
         ("max_delay", C.c_uint32),
         ("keys", C.c_uint32),
         ("steps_per_launch", C.c_uint32),
+        ("history", C.c_uint32),
         ("device", C.c_int32),
         ("clusters", C.c_uint64),
         ("cluster_base", C.c_uint64),
@@ -154,8 +155,8 @@ def declare(lib, prefix):
 
 def make_config(npz=(5,), protocol=PAXOS, q1=Q_MAJORITY, q2=Q_MAJORITY, fz=0, thrifty=0,
                 ephemeral_leader=0, reply_when_commit=0, adaptive=1, policy_threshold=3,
-                window=32, mbox_cap=16, max_delay=4, keys=16, steps_per_launch=0, device=0,
-                clusters=1, cluster_base=0, seed=1):
+                window=16, mbox_cap=16, max_delay=4, keys=16, steps_per_launch=0, device=0,
+                clusters=1, cluster_base=0, seed=1, history=0):
     c = Config()
     c.protocol = protocol
     c.n_zones = len(npz)
@@ -165,7 +166,7 @@ def make_config(npz=(5,), protocol=PAXOS, q1=Q_MAJORITY, q2=Q_MAJORITY, fz=0, th
     c.thrifty, c.ephemeral_leader, c.reply_when_commit = thrifty, ephemeral_leader, reply_when_commit
     c.adaptive, c.policy_threshold = adaptive, policy_threshold
     c.window, c.mbox_cap, c.max_delay, c.keys = window, mbox_cap, max_delay, keys
-    c.steps_per_launch, c.device = steps_per_launch, device
+    c.steps_per_launch, c.device, c.history = steps_per_launch, device, history
     c.clusters, c.cluster_base, c.seed = clusters, cluster_base, seed
     return c
 

@@ -12,6 +12,8 @@
 #include <utility>
 #include <vector>
 
+#include "abd_kernel.h"
+#include "lin_kernel.h"
 #include "paxisim_dev.h"
 #include "paxos_kernel.h"
 
@@ -50,6 +52,8 @@ struct paxisim {
   double kernel_ms = 0;
   uint64_t launches = 0;
 };
+
+static inline size_t rc_host(const Params& P, uint32_t r, uint64_t c) { return (size_t)r * P.C + c; }
 
 extern "C" int paxisim_abi_version(void) { return PAXISIM_ABI_VERSION; }
 extern "C" const char* paxisim_last_error(void) { return g_err; }
@@ -129,6 +133,28 @@ __global__ void gather_kernel(Params P, uint64_t lo, uint64_t n, paxisim_replica
   s.discarded = P.stats[krc(P, ST_DISCARDED, r, c)];
   s.commits = P.stats[krc(P, ST_COMMITS, r, c)];
   s.replies = P.stats[krc(P, ST_REPLIES, r, c)];
+  if (P.protocol == PAXISIM_ABD) {   // op counter, Done ops recorded, KV digest, live ops
+    const uint8_t* img = P.image + (c / LANES) * (size_t)P.img.bytes;
+    const uint32_t lane = (uint32_t)(c % LANES);
+    const uint32_t* kv_val = reinterpret_cast<const uint32_t*>(img + P.img.off_a);
+    const uint32_t* kv_ver = reinterpret_cast<const uint32_t*>(img + P.img.off_b);
+    const uint32_t* ops = reinterpret_cast<const uint32_t*>(img + P.img.off_c);
+    uint64_t d = 0;
+    for (uint32_t k = 0; k < P.keys; k++) {
+      const uint32_t ki = ((r * P.keys + k) << 6) | lane;
+      d = mix64(d ^ (((uint64_t)kv_ver[ki] << 32) | kv_val[ki]));
+    }
+    uint32_t live = 0;
+    for (uint32_t k = 0; k < P.OW; k++) {
+      const uint32_t st = ops[(((r * P.OW + k) * ABD_OPF + 2) << 6) | lane] & 3u;
+      live += st == ABD_GET || st == ABD_SET;
+    }
+    s.ballot = 0;
+    s.active = 0;
+    s.p1_acks = 0;
+    s.digest = d;
+    s.npending = live;
+  }
   out[i] = s;
 }
 
@@ -158,16 +184,28 @@ __global__ void check_kernel(Params P, uint64_t* out) {
 // ---------------------------------------------------------------------------
 // C-ABI
 // ---------------------------------------------------------------------------
+static Image proto_image(uint32_t protocol, uint32_t N, uint32_t W, uint32_t K, uint32_t WK, uint32_t D) {
+  if (protocol == PAXISIM_ABD) {
+    const uint32_t kv = N * K * LANES * 4u;
+    return image_layout(kv, kv, N * abd_ow(WK) * ABD_OPF * LANES * 4u, N, WK, D);
+  }
+  const uint32_t logb = N * W * LANES * 4u;
+  return image_layout(logb, logb, logb, N, WK, D);
+}
+
 static int check_config(const paxisim_config* cfg, const paxisim_workload* wl, const paxisim_fault_process* fp,
                         uint32_t* N_out) {
   uint32_t N = 0;
-  if (cfg->protocol != PAXISIM_PAXOS) return fail(PAXISIM_EUNSUPP, "protocol %u not built", cfg->protocol);
+  if (cfg->protocol != PAXISIM_PAXOS && cfg->protocol != PAXISIM_ABD)
+    return fail(PAXISIM_EUNSUPP, "protocol %u not built", cfg->protocol);
+  if (cfg->protocol == PAXISIM_ABD && (cfg->keys < 1 || cfg->keys > 64)) return fail(PAXISIM_EINVAL, "keys");
   if (cfg->n_zones < 1 || cfg->n_zones > PAXISIM_MAX_ZONES) return fail(PAXISIM_EINVAL, "n_zones");
   for (uint32_t z = 0; z < cfg->n_zones; z++) {
     if (cfg->npz[z] < 1) return fail(PAXISIM_EINVAL, "npz[%u] must be >= 1", z);
     N += cfg->npz[z];
   }
   if (N < 1 || N > PAXISIM_MAX_N) return fail(PAXISIM_EINVAL, "N=%u out of range", N);
+  if (cfg->protocol == PAXISIM_ABD && N > 15) return fail(PAXISIM_EINVAL, "ABD supports N <= 15");
   if (cfg->window < 8 || cfg->window > PAXISIM_MAX_WINDOW || (cfg->window & (cfg->window - 1)))
     return fail(PAXISIM_EINVAL, "window must be a power of 2 in [8,64]");
   if (cfg->mbox_cap < 2 || cfg->mbox_cap > PAXISIM_MAX_MBOX) return fail(PAXISIM_EINVAL, "mbox_cap");
@@ -180,7 +218,7 @@ static int check_config(const paxisim_config* cfg, const paxisim_workload* wl, c
     if (wl->target[w] >= N) return fail(PAXISIM_EINVAL, "target[%u]", w);
   if (fp->slow_ppm && (fp->slow_min > fp->slow_max || fp->slow_max > cfg->max_delay))
     return fail(PAXISIM_EINVAL, "slow delay range exceeds max_delay");
-  const Image img = image_layout(N, cfg->window, wl->outstanding, cfg->max_delay + 2u);
+  const Image img = proto_image(cfg->protocol, N, cfg->window, cfg->keys, wl->outstanding, cfg->max_delay + 2u);
   if (img.bytes > LDS_MAX)
     return fail(PAXISIM_EUNSUPP, "workgroup image %u B exceeds LDS (%u B): reduce window/max_delay/replicas",
                 img.bytes, LDS_MAX);
@@ -243,8 +281,13 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
   h->S = cfg->steps_per_launch ? cfg->steps_per_launch : 32;
   Params& P = h->P;
   memset(&P, 0, sizeof P);
+  P.protocol = cfg->protocol;
   P.N = N;
   P.Z = cfg->n_zones;
+  P.keys = cfg->keys ? cfg->keys : 1;
+  P.write_ppm = wl->write_ppm;
+  P.H = cfg->protocol == PAXISIM_ABD ? cfg->history : 0;
+  P.OW = abd_ow(wl->outstanding);
   P.W = cfg->window;
   P.M = cfg->mbox_cap;
   P.D = cfg->max_delay + 2u;
@@ -280,7 +323,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
   for (uint32_t w = 0; w < PAXISIM_MAX_WORKERS; w++) P.target[w] = wl->target[w];
 
   const size_t C = P.C, NC = (size_t)N * C, blocks = C / LANES;
-  P.img = image_layout(N, P.W, P.WK, P.D);
+  P.img = proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D);
   P.rec_per_block = P.D * N * P.NS * P.M * LANES;
   // size the arena (rec last: it is the only region not zeroed)
   size_t zero_bytes = 0, total = 0;
@@ -295,6 +338,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     uint64_t* ckd = carve<uint64_t>(p, NC * CKR);
     uint32_t* st = carve<uint32_t>(p, NC * NSTAT);
     uint32_t* reqx = carve<uint32_t>(p, NC * P.W);
+    uint4* hist = carve<uint4>(p, NC * P.H);
     uint8_t* image = carve<uint8_t>(p, blocks * P.img.bytes);
     char* zend = p;
     uint4* rec = carve<uint4>(p, blocks * P.rec_per_block);
@@ -303,7 +347,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
       P.flags = s7 + 4 * NC; P.npend = s7 + 5 * NC; P.nfwd = s7 + 6 * NC;
       P.digest = dg; P.kc = kc; P.pend = pend; P.fwd = fwd;
       P.link_drop = links; P.link_slow = links + NC * N;
-      P.ck_e = cke; P.ck_d = ckd; P.stats = st; P.reqx = reqx; P.image = image; P.rec = rec;
+      P.ck_e = cke; P.ck_d = ckd; P.stats = st; P.reqx = reqx; P.hist = hist; P.image = image; P.rec = rec;
     }
     return std::make_pair((size_t)zend, (size_t)p);
   };
@@ -355,19 +399,35 @@ extern "C" int paxisim_fault_add(paxisim* h, const paxisim_fault* f) {
   return 0;
 }
 
-template <int NT>
+template <int NT, class Proto>
 static hipError_t launch_steps(paxisim* h, uint32_t t0, uint32_t n) {
   const Params& P = h->P;
   const unsigned grid = (unsigned)(P.C / LANES);
   static thread_local bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&paxos_steps<NT>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sim_steps<NT, Proto>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  paxos_steps<NT><<<grid, P.N * LANES, P.img.bytes, h->stream>>>(P, t0, n);
+  sim_steps<NT, Proto><<<grid, P.N * LANES, P.img.bytes, h->stream>>>(P, t0, n);
   return hipGetLastError();
+}
+
+static hipError_t launch_any(paxisim* h, uint32_t t0, uint32_t n) {
+  if (h->P.protocol == PAXISIM_ABD) {
+    switch (h->P.N) {
+      case 3: return launch_steps<3, AbdProto>(h, t0, n);
+      case 5: return launch_steps<5, AbdProto>(h, t0, n);
+      default: return launch_steps<0, AbdProto>(h, t0, n);
+    }
+  }
+  switch (h->P.N) {
+    case 3: return launch_steps<3, PaxosProto>(h, t0, n);
+    case 5: return launch_steps<5, PaxosProto>(h, t0, n);
+    case 9: return launch_steps<9, PaxosProto>(h, t0, n);
+    default: return launch_steps<0, PaxosProto>(h, t0, n);
+  }
 }
 
 extern "C" int paxisim_step(paxisim* h, uint32_t nsteps) {
@@ -380,13 +440,7 @@ extern "C" int paxisim_step(paxisim* h, uint32_t nsteps) {
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
     HIPCHK(hipEventRecord(a, h->stream));
-    hipError_t le;
-    switch (h->P.N) {
-      case 3: le = launch_steps<3>(h, h->t, n); break;
-      case 5: le = launch_steps<5>(h, h->t, n); break;
-      case 9: le = launch_steps<9>(h, h->t, n); break;
-      default: le = launch_steps<0>(h, h->t, n); break;
-    }
+    const hipError_t le = launch_any(h, h->t, n);
     if (le != hipSuccess) return fail(PAXISIM_EDEVICE, "step launch: %s", hipGetErrorString(le));
     HIPCHK(hipEventRecord(b, h->stream));
     h->evs.emplace_back(a, b);
@@ -486,5 +540,79 @@ extern "C" int paxisim_check(paxisim* h, uint64_t* violations) {
 extern "C" int paxisim_device_bytes(paxisim* h, uint64_t* bytes) {
   if (!h || !bytes) return fail(PAXISIM_EINVAL, "null argument");
   *bytes = h->arena_bytes;
+  return 0;
+}
+
+// Completed ABD operations of one cluster, 5 words per op {key, is_write,
+// value, start, end}, replicas in index order, each in completion order.
+extern "C" int paxisim_history(paxisim* h, uint64_t cluster, uint32_t* buf, uint32_t cap_ops, uint32_t* n_out) {
+  if (!h || !n_out) return fail(PAXISIM_EINVAL, "null argument");
+  if (cluster >= h->cfg.clusters) return fail(PAXISIM_ERANGE, "cluster");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const Params& P = h->P;
+  std::vector<uint32_t> len(P.N);
+  for (uint32_t r = 0; r < P.N; r++)
+    HIPCHK(hipMemcpy(&len[r], &P.execute[rc_host(P, r, cluster)], 4, hipMemcpyDeviceToHost));
+  uint32_t n = 0;
+  for (uint32_t r = 0; r < P.N && P.H; r++) {
+    std::vector<uint4> tmp(len[r]);
+    if (len[r])
+      HIPCHK(hipMemcpy(tmp.data(), &P.hist[((size_t)r * P.C + cluster) * P.H], len[r] * sizeof(uint4),
+                       hipMemcpyDeviceToHost));
+    for (uint32_t j = 0; j < len[r]; j++, n++) {
+      if (!buf || n >= cap_ops) continue;
+      uint32_t* o = buf + 5 * (size_t)n;
+      o[0] = tmp[j].x & 0x7FFFFFFFu;
+      o[1] = tmp[j].x >> 31;
+      o[2] = tmp[j].y;
+      o[3] = tmp[j].z;
+      o[4] = tmp[j].w;
+    }
+  }
+  *n_out = n;
+  return 0;
+}
+
+extern "C" int paxisim_linearizable(paxisim* h, uint64_t* anomalies, uint64_t* ops, uint64_t* skipped) {
+  if (!h) return fail(PAXISIM_EINVAL, "null handle");
+  if (h->P.protocol != PAXISIM_ABD || h->P.H == 0)
+    return fail(PAXISIM_EUNSUPP, "linearizability scan needs protocol ABD with history > 0");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const Params& P = h->P;
+  // per-thread workspace, one chunk of (cluster, key) partitions at a time
+  const uint64_t total = P.clusters * P.keys;
+  const uint64_t T = total < (1ull << 18) ? (total + 63) / 64 * 64 : (1ull << 18);
+  const size_t per = (size_t)LIN_MAXV * (LIN_WORDS * 8 + 7 * 4);
+  char* ws_mem = nullptr;
+  HIPCHK(hipMalloc(&ws_mem, per * T));
+  LinWs ws;
+  {
+    char* p = ws_mem;
+    ws.adj = reinterpret_cast<uint64_t*>(p); p += (size_t)LIN_MAXV * LIN_WORDS * 8 * T;
+    ws.vin = reinterpret_cast<uint32_t*>(p); p += (size_t)LIN_MAXV * 4 * T;
+    ws.vout = reinterpret_cast<uint32_t*>(p); p += (size_t)LIN_MAXV * 4 * T;
+    ws.vstart = reinterpret_cast<uint32_t*>(p); p += (size_t)LIN_MAXV * 4 * T;
+    ws.vend = reinterpret_cast<uint32_t*>(p); p += (size_t)LIN_MAXV * 4 * T;
+    ws.vw = reinterpret_cast<uint32_t*>(p); p += (size_t)LIN_MAXV * 4 * T;
+    ws.order = reinterpret_cast<uint32_t*>(p); p += (size_t)LIN_MAXV * 4 * T;
+    ws.stk = reinterpret_cast<uint32_t*>(p);
+    ws.T = T;
+  }
+  hipError_t e = hipMemsetAsync(h->d_scratch, 0, 3 * sizeof(uint64_t), h->stream);
+  const uint64_t per_chunk = T / P.keys;
+  for (uint64_t c0 = 0; e == hipSuccess && c0 < P.clusters; c0 += per_chunk) {
+    const uint64_t nc = (P.clusters - c0) < per_chunk ? (P.clusters - c0) : per_chunk;
+    const uint64_t threads = nc * P.keys;
+    lin_kernel<<<(unsigned)((threads + 63) / 64), 64, 0, h->stream>>>(P, ws, c0, nc, h->d_scratch);
+    e = hipGetLastError();
+  }
+  uint64_t res[3] = {0, 0, 0};
+  if (e == hipSuccess) e = hipMemcpyAsync(res, h->d_scratch, sizeof res, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(ws_mem);
+  if (e != hipSuccess) return fail(PAXISIM_EDEVICE, "linearizable: %s", hipGetErrorString(e));
+  if (anomalies) *anomalies = res[0];
+  if (ops) *ops = res[1];
+  if (skipped) *skipped = res[2];
   return 0;
 }

@@ -45,17 +45,20 @@ enum {
 };
 
 // Byte layout of a workgroup's LDS image (identical in HBM, one per block).
+// Regions a/b/c belong to the protocol:
+//   Paxos: log window ballot / cmd|flags / ack mask, each [r][W][lane] u32
+//   ABD:   KV value / KV version [r][K][lane] u32, op table [r][OW][6][lane] u32
 struct Image {
-  uint32_t off_bal, off_cmd, off_ack, off_wcur, off_wiss, off_poison, off_cnt, bytes;
+  uint32_t off_a, off_b, off_c, off_wcur, off_wiss, off_poison, off_cnt, bytes;
 };
 
-__host__ __device__ inline Image image_layout(uint32_t N, uint32_t W, uint32_t WK, uint32_t D) {
+__host__ __device__ inline Image image_layout(uint32_t bytes_a, uint32_t bytes_b, uint32_t bytes_c, uint32_t N,
+                                              uint32_t WK, uint32_t D) {
   Image m;
-  const uint32_t logb = N * W * LANES * 4u;
-  m.off_bal = 0;
-  m.off_cmd = m.off_bal + logb;
-  m.off_ack = m.off_cmd + logb;
-  m.off_wcur = m.off_ack + logb;
+  m.off_a = 0;
+  m.off_b = m.off_a + bytes_a;
+  m.off_c = m.off_b + bytes_b;
+  m.off_wcur = m.off_c + bytes_c;
   m.off_wiss = m.off_wcur + WK * LANES * 4u;
   m.off_poison = m.off_wiss + WK * LANES * 4u;
   m.off_cnt = m.off_poison + LANES * 4u;
@@ -63,8 +66,18 @@ __host__ __device__ inline Image image_layout(uint32_t N, uint32_t W, uint32_t W
   return m;
 }
 
+// ABD op table: a power of two >= 2*outstanding, at least 4
+__host__ __device__ inline uint32_t abd_ow(uint32_t outstanding) {
+  uint32_t ow = 4;
+  while (ow < 2u * outstanding) ow <<= 1;
+  return ow;
+}
+constexpr uint32_t ABD_OPF = 6;   // op fields: tag, req, state|get<<2|set<<17, value, version, start
+enum { ABD_FREE = 0, ABD_GET = 1, ABD_SET = 2, ABD_DONE = 3 };
+
 struct Params {
-  uint32_t N, Z, W, M, D, NS, WK, max_requests;
+  uint32_t protocol, N, Z, W, M, D, NS, WK, max_requests;
+  uint32_t keys, write_ppm, H, OW;
   uint64_t C;            // allocated cluster lanes (multiple of 64)
   uint64_t clusters;     // live clusters
   uint64_t cluster_base, seed;
@@ -85,7 +98,8 @@ struct Params {
   uint32_t* ck_e;        // [CKR][N][C]
   uint64_t* ck_d;        // [CKR][N][C]
   uint32_t* stats;       // [NSTAT][N][C]
-  uint32_t* reqx;        // [blk][N][W][64] request side table
+  uint32_t* reqx;        // [blk][N][W][64] request side table (Paxos)
+  uint4* hist;           // [N][C][H] completed ABD ops {key|write<<31, value, start, end}
   uint8_t* image;        // [blk][img.bytes]
   uint4* rec;            // [blk][D][dst][src][M][64]
 };

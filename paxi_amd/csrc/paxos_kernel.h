@@ -1,59 +1,17 @@
-// paxos_kernel.h — Multi-Paxos replica step on gfx950 (LDS-resident workgroup).
+// paxos_kernel.h — Multi-Paxos handlers on gfx950 (a protocol policy of sim_core.h).
 //
 // One lane = one replica of one cluster.  The handlers follow
-// paxos/paxos.go:86-376 and paxos/replica.go:42-66 (cited per function), the
-// socket filter socket.go:66-109 and the node runtime node.go:79-172, under
-// the delivery schedule of DESIGN.md §3.
+// paxos/paxos.go:86-376 and paxos/replica.go:42-66 (cited per function) and the
+// node runtime's forward/reply routing node.go:79-172.
 //
-// Memory map during a launch:
-//   registers: replica scalars (ballot, slot, execute, active, p1 acks, flags,
-//              digest, counters) and the socket fault state of the N links
-//   LDS:       log windows {ballot, cmd|flags, acks} [r][W][lane], mailbox
-//              counts [bucket][dst][src][lane], client workers, poison step
-//   HBM:       message records (block-contiguous, prefetched one ahead),
-//              request side table, pending/forward tables, checkpoints
+// Paxos state during a launch:
+//   registers: ballot, slot, execute, active, phase-1 acks, pending/forward counts, digest
+//   LDS:       log window {ballot, cmd|flags, acks} as [r][W][lane] u32 (regions a, b, c)
+//   HBM:       request side table, pending/forward tables, digest checkpoints
 #pragma once
-#include "paxisim_dev.h"
+#include "sim_core.h"
 
 namespace pxs {
-
-template <int NT>
-struct Rep {
-  static constexpr uint32_t NL = NT ? (uint32_t)NT : (uint32_t)PAXISIM_MAX_N;  // link registers
-  uint64_t c, gid;                      // global lane / cluster id
-  uint32_t lane, r, t, b0, hs, kc, blk;
-  uint32_t ballot;
-  int32_t slot, execute;
-  uint32_t active, p1mask, flags, npend, nfwd;
-  uint64_t digest;
-  uint32_t du[NL], su[NL];              // link fault state: drop_until; slow_until | delay << 28
-  uint32_t dv[9];                       // delivered by type (REQUEST..P3)
-  uint32_t client, sent, dropped, discarded, commits, replies;
-  uint32_t send_seq;
-  bool stop, crashed;
-  // LDS views
-  uint32_t *l_bal, *l_cmd, *l_ack, *l_wcur, *l_wiss, *l_poison;
-  uint8_t* l_cnt;
-  uint4* rec;                           // this block's record region
-};
-
-template <int NT>
-__device__ __forceinline__ uint32_t nrep(const Params& P) { return NT ? (uint32_t)NT : P.N; }
-
-// register-array select / update with a runtime index (unrolled: no scratch)
-// (the empty asm keeps LLVM from folding the select chain back into an
-// alloca + dynamic index, which would put the array in scratch memory)
-__device__ __forceinline__ uint32_t opaque(uint32_t v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
-template <int NT>
-__device__ __forceinline__ uint32_t lsel(const uint32_t (&a)[Rep<NT>::NL], uint32_t i) {
-  uint32_t v = opaque(a[0]);
-#pragma unroll
-  for (uint32_t k = 1; k < Rep<NT>::NL; k++) v = (i == k) ? opaque(a[k]) : v;
-  return v;
-}
 
 // ---------------------------------------------------------------------------
 // log window in LDS: entry of slot s of replica r at [(r*W + (s & (W-1)))*64 + lane]
@@ -65,12 +23,12 @@ __device__ __forceinline__ uint32_t eidx(const Params& P, const Rep<NT>& x, int3
   return ((x.r * P.W + ((uint32_t)s & (P.W - 1u))) << 6) | x.lane;
 }
 template <int NT>
-__device__ __forceinline__ Ent eget(const Rep<NT>& x, uint32_t i) { return Ent{x.l_bal[i], x.l_cmd[i], x.l_ack[i]}; }
+__device__ __forceinline__ Ent eget(const Rep<NT>& x, uint32_t i) { return Ent{x.l_a[i], x.l_b[i], x.l_c[i]}; }
 template <int NT>
 __device__ __forceinline__ void eput(Rep<NT>& x, uint32_t i, const Ent& e) {
-  x.l_bal[i] = e.b;
-  x.l_cmd[i] = e.c;
-  x.l_ack[i] = e.a;
+  x.l_a[i] = e.b;
+  x.l_b[i] = e.c;
+  x.l_c[i] = e.a;
 }
 // request side table slot for LDS entry index i
 template <int NT>
@@ -103,100 +61,8 @@ __device__ __forceinline__ uint32_t eset_cmd(const Params& P, const Rep<NT>& x, 
 }
 
 // ---------------------------------------------------------------------------
-// socket.Send (socket.go:66-109): crash -> drop -> flaky -> slow, then the
-// bounded (link, arrival-step) bucket.  Returns the record index to write.
+// Request.Reply routing (node.go:83-97) and node.Forward (node.go:165-172)
 // ---------------------------------------------------------------------------
-template <int NT>
-__device__ __forceinline__ bool send_begin(const Params& P, Rep<NT>& x, uint32_t to, uint32_t nrec, uint32_t& ri) {
-  const uint32_t N = nrep<NT>(P);
-  const uint32_t seq = x.send_seq++;
-  x.sent++;
-  if (to >= N || x.crashed) { x.dropped++; return false; }
-  if (x.t < lsel<NT>(x.du, to) || (P.nfaults && scripted(P, PAXISIM_FAULT_DROP, x.gid, x.r, to, x.t, nullptr))) {
-    x.dropped++;
-    return false;
-  }
-  uint32_t delay = 0;
-  if (P.nfaults) {
-    uint32_t p = 0;
-    if (scripted(P, PAXISIM_FAULT_FLAKY, x.gid, x.r, to, x.t, &p) && p > 0 &&
-        ppm_hit(draw(x.hs, tag(PUR_FLAKY, x.r, seq)), p)) {
-      x.dropped++;
-      return false;
-    }
-  }
-  const uint32_t su = lsel<NT>(x.su, to);
-  if (x.t < (su & (T_MAX - 1u))) delay = su >> 28;
-  if (P.nfaults) scripted(P, PAXISIM_FAULT_SLOW, x.gid, x.r, to, x.t, &delay);
-  if (delay > P.max_delay) delay = P.max_delay;
-  uint32_t b = x.b0 + 1u + delay;
-  if (b >= P.D) b -= P.D;
-  const uint32_t box = (b * N + to) * P.NS + x.r;
-  uint8_t* cp = &x.l_cnt[(box << 6) | x.lane];
-  const uint32_t k = *cp;
-  if (k + nrec > P.M) {
-    x.flags |= PAXISIM_F_MBOX_OVF | PAXISIM_F_UNFAITHFUL;
-    x.dropped++;
-    return false;
-  }
-  *cp = (uint8_t)(k + nrec);
-  ri = ((box * P.M + k) << 6) | x.lane;
-  return true;
-}
-
-template <int NT>
-__device__ __forceinline__ void send1(const Params& P, Rep<NT>& x, uint32_t to, uint32_t type, uint32_t ballot,
-                                      uint32_t slot, uint32_t cid) {
-  uint32_t ri;
-  if (send_begin<NT>(P, x, to, 1, ri)) x.rec[ri] = make_uint4(type, ballot, slot, cid);
-}
-
-// Broadcast: every peer except self, IDs.Less order (socket.go:147-155; G1, G2)
-template <int NT>
-__device__ __forceinline__ void broadcast1(const Params& P, Rep<NT>& x, uint32_t type, uint32_t ballot,
-                                           uint32_t slot, uint32_t cid) {
-  const uint32_t N = nrep<NT>(P);
-#pragma nounroll
-  for (uint32_t d = 0; d < N; d++)
-    if (d != x.r) send1<NT>(P, x, d, type, ballot, slot, cid);
-}
-
-// ---------------------------------------------------------------------------
-// client (benchmark.go:246-275) and Request.Reply routing (node.go:83-97)
-// ---------------------------------------------------------------------------
-template <int NT>
-__device__ __forceinline__ void client_reply(const Params& P, Rep<NT>& x, uint32_t cid) {
-  const uint32_t w = (cid - 1u) % P.WK;
-  const uint32_t wi = (w << 6) | x.lane;
-  if (x.l_wcur[wi] != cid) return;              // duplicate reply: the worker moved on
-  x.replies++;
-  const uint32_t issued = x.l_wiss[wi];
-  if (P.max_requests == 0 || issued < P.max_requests) {
-    const uint64_t nc = 1ull + w + (uint64_t)P.WK * issued;
-    if (nc > CMD_MASK) {
-      x.flags |= PAXISIM_F_PEND_OVF | PAXISIM_F_UNFAITHFUL;
-      x.l_wcur[wi] = 0;
-      return;
-    }
-    x.l_wiss[wi] = issued + 1u;
-    x.l_wcur[wi] = (uint32_t)nc;
-    // the next request reaches the worker's target next step (client source N)
-    uint32_t b = x.b0 + 1u;
-    if (b >= P.D) b -= P.D;
-    const uint32_t box = (b * nrep<NT>(P) + P.target[w]) * P.NS + nrep<NT>(P);
-    uint8_t* cp = &x.l_cnt[(box << 6) | x.lane];
-    const uint32_t k = *cp;
-    if (k >= P.M) {
-      x.flags |= PAXISIM_F_MBOX_OVF | PAXISIM_F_UNFAITHFUL;
-      return;
-    }
-    x.rec[((box * P.M + k) << 6) | x.lane] = make_uint4(PAXISIM_MSG_REQUEST, 0u, 0u, (uint32_t)nc);
-    *cp = (uint8_t)(k + 1u);
-  } else {
-    x.l_wcur[wi] = 0;
-  }
-}
-
 template <int NT>
 __device__ __forceinline__ void request_reply(const Params& P, Rep<NT>& x, uint32_t req, uint32_t reply_cmd) {
   const uint32_t o = req_origin(req);
@@ -303,13 +169,13 @@ template <int NT>
 __device__ __forceinline__ void paxos_exec(const Params& P, Rep<NT>& x) {     // paxos.go:345-369
   for (;;) {
     const uint32_t i = eidx<NT>(P, x, x.execute);
-    const uint32_t c = x.l_cmd[i];
+    const uint32_t c = x.l_b[i];
     if ((c & (EF_EXISTS | EF_COMMIT)) != (EF_EXISTS | EF_COMMIT)) break;
     if (x.flags & PAXISIM_F_WOVF) x.flags |= PAXISIM_F_UNFAITHFUL;
     const uint32_t cmd = c & CMD_MASK;
     if (c & (EF_REQSELF | EF_REQEXT)) request_reply<NT>(P, x, ereq<NT>(P, x, i, c), cmd);
     x.digest = mix64(x.digest ^ (((uint64_t)(uint32_t)x.execute << 32) | cmd));
-    x.l_cmd[i] = 0u;                                                 // delete(p.log, execute)
+    x.l_b[i] = 0u;                                                 // delete(p.log, execute)
     x.execute++;
     if ((uint32_t)x.execute % CKI == 0) {
       const uint32_t k = ((uint32_t)x.execute / CKI) % CKR;
@@ -331,7 +197,7 @@ __device__ __forceinline__ void paxos_handle_p1a(const Params& P, Rep<NT>& x, ui
   if (hi > x.execute + (int32_t)P.W - 1) hi = x.execute + (int32_t)P.W - 1;
   uint32_t n = 0;
   for (int32_t s = x.execute; s <= hi; s++) {
-    const uint32_t c = x.l_cmd[eidx<NT>(P, x, s)];
+    const uint32_t c = x.l_b[eidx<NT>(P, x, s)];
     n += (c & EF_EXISTS) && !(c & EF_COMMIT);
   }
   uint32_t ri;
@@ -386,11 +252,11 @@ __device__ __forceinline__ void paxos_handle_p1b(const Params& P, Rep<NT>& x, ui
       if (hi > x.execute + (int32_t)P.W - 1) hi = x.execute + (int32_t)P.W - 1;
       for (int32_t s = x.execute; s <= hi; s++) {
         const uint32_t i = eidx<NT>(P, x, s);
-        const uint32_t c = x.l_cmd[i];
+        const uint32_t c = x.l_b[i];
         if (!(c & EF_EXISTS) || (c & EF_COMMIT)) continue;                   // nil gap (G5)
-        x.l_bal[i] = x.ballot;
-        x.l_cmd[i] = c | EF_QUORUM;
-        x.l_ack[i] = 1u << x.r;
+        x.l_a[i] = x.ballot;
+        x.l_b[i] = c | EF_QUORUM;
+        x.l_c[i] = 1u << x.r;
         broadcast1<NT>(P, x, PAXISIM_MSG_P2A, x.ballot, (uint32_t)s, c & CMD_MASK);
       }
       const uint32_t np = x.npend;
@@ -418,8 +284,8 @@ __device__ __forceinline__ void paxos_handle_p2a(const Params& P, Rep<NT>& x, ui
           }
           e.c = eset_cmd<NT>(P, x, i, e.c, mcid);
           e.b = mb;
-          x.l_bal[i] = e.b;
-          x.l_cmd[i] = e.c;
+          x.l_a[i] = e.b;
+          x.l_b[i] = e.c;
         }
       } else {
         eput<NT>(x, i, Ent{mb, mcid | EF_EXISTS, 0u});
@@ -442,8 +308,8 @@ __device__ __forceinline__ void paxos_handle_p2b(const Params& P, Rep<NT>& x, ui
     return;
   }
   const uint32_t i = eidx<NT>(P, x, ms);
-  const uint32_t c = x.l_cmd[i];
-  const uint32_t eb = x.l_bal[i];
+  const uint32_t c = x.l_b[i];
+  const uint32_t eb = x.l_a[i];
   if (!(c & EF_EXISTS) || mb < eb || (c & EF_COMMIT)) return;
   if (mb > x.ballot) {
     x.ballot = mb;
@@ -455,10 +321,10 @@ __device__ __forceinline__ void paxos_handle_p2b(const Params& P, Rep<NT>& x, ui
       x.stop = true;
       return;
     }
-    const uint32_t ack = x.l_ack[i] | (1u << src);
-    x.l_ack[i] = ack;
+    const uint32_t ack = x.l_c[i] | (1u << src);
+    x.l_c[i] = ack;
     if (quorum_ok(P, P.q2, ack)) {
-      x.l_cmd[i] = c | EF_COMMIT;
+      x.l_b[i] = c | EF_COMMIT;
       x.commits++;
       broadcast1<NT>(P, x, PAXISIM_MSG_P3, mb, (uint32_t)ms, c & CMD_MASK);
       if (P.rwc) {
@@ -478,7 +344,7 @@ __device__ __forceinline__ void paxos_handle_p3(const Params& P, Rep<NT>& x, uin
   if (ms > x.slot) x.slot = ms;
   if (in_window<NT>(P, x, ms)) {
     const uint32_t i = eidx<NT>(P, x, ms);
-    uint32_t c = x.l_cmd[i];
+    uint32_t c = x.l_b[i];
     if (c & EF_EXISTS) {
       if ((c & CMD_MASK) != mcid && (c & (EF_REQSELF | EF_REQEXT))) {
         node_forward<NT>(P, x, bal_id(mb), ereq<NT>(P, x, i, c));
@@ -486,11 +352,11 @@ __device__ __forceinline__ void paxos_handle_p3(const Params& P, Rep<NT>& x, uin
       }
     } else {
       c = EF_EXISTS;                                                          // &entry{} (G6)
-      x.l_bal[i] = 0u;
-      x.l_ack[i] = 0u;
+      x.l_a[i] = 0u;
+      x.l_c[i] = 0u;
     }
     c = eset_cmd<NT>(P, x, i, c, mcid) | EF_COMMIT;
-    x.l_cmd[i] = c;
+    x.l_b[i] = c;
     if (P.rwc) {
       if (c & (EF_REQSELF | EF_REQEXT)) {
         const uint32_t q = ereq<NT>(P, x, i, c);
@@ -507,218 +373,52 @@ __device__ __forceinline__ void paxos_handle_p3(const Params& P, Rep<NT>& x, uin
 }
 
 // ---------------------------------------------------------------------------
-// One replica, one step
+// protocol policy
 // ---------------------------------------------------------------------------
-template <int NT>
-__device__ __forceinline__ void fault_process(const Params& P, Rep<NT>& x) {
-  if (P.drop_ppm == 0 && P.slow_ppm == 0) return;
-#pragma unroll
-  for (uint32_t d = 0; d < Rep<NT>::NL; d++) {
-    if (d >= nrep<NT>(P) || d == x.r) continue;
-    const uint32_t u = draw(x.hs, tag(PUR_LINK, x.r, d));
-    if (P.drop_ppm && x.t >= x.du[d] && ppm_hit16(u & 0xFFFFu, P.drop_ppm)) x.du[d] = x.t + P.drop_len;
-    if (P.slow_ppm && x.t >= (x.su[d] & (T_MAX - 1u)) && ppm_hit16(u >> 16, P.slow_ppm)) {
-      const uint32_t span = P.slow_max - P.slow_min + 1u;
-      const uint32_t v = draw(x.hs, tag(PUR_SLOWD, x.r, d));
-      x.su[d] = (x.t + P.slow_len) | ((P.slow_min + __umulhi(v, span)) << 28);
-    }
-  }
-}
-
-template <int NT>
-__device__ __forceinline__ void paxos_replica_step(const Params& P, Rep<NT>& x) {
-  constexpr uint32_t NSMAX = NT ? (uint32_t)NT + 1u : (uint32_t)PAXISIM_MAX_N + 1u;
-  const uint32_t N = nrep<NT>(P), NS = N + 1u;
-  x.send_seq = 0;
-  x.stop = false;
-  x.hs = step_key(x.kc, x.t);
-  fault_process<NT>(P, x);
-  x.crashed = P.nfaults && scripted(P, PAXISIM_FAULT_CRASH, x.gid, x.r, 0u, x.t, nullptr);
-
-  const uint32_t box0 = (x.b0 * N + x.r) * NS;          // inbox boxes: box0 + src
-  uint32_t rem[NSMAX], pos[NSMAX], total = 0;
-#pragma unroll
-  for (uint32_t s = 0; s < NSMAX; s++) {
-    rem[s] = 0;
-    pos[s] = 0;
-    if (s < NS) {
-      uint32_t n = x.l_cnt[((box0 + s) << 6) | x.lane];
-      if (x.crashed && s < N && n) {                    // socket.Recv discards (socket.go:111-118)
-        for (uint32_t k = 0; k < n;) {
-          const uint32_t h = x.rec[(((box0 + s) * P.M + k) << 6) | x.lane].x;
-          x.discarded++;
-          k += 1u + (hdr_type(h) == PAXISIM_MSG_P1B ? hdr_n(h) : 0u);
-        }
-        n = 0;
-      }
-      rem[s] = n;
-      total += n;
-    }
-  }
-
-  // merge order: weighted pick among sources, two 16-bit picks per draw;
-  // the next message's record is loaded before the current one is handled
-  uint32_t u = 0, i = 0, src = 0, ri = 0;
-  uint4 m = make_uint4(0u, 0u, 0u, 0u);
-  auto pick = [&](uint32_t idx, uint32_t& psrc, uint32_t& pri) {
-    if (!(idx & 1u)) u = draw(x.hs, tag(PUR_ORDER, x.r, idx >> 1));
-    uint32_t pk = (((idx & 1u) ? (u >> 16) : (u & 0xFFFFu)) * total) >> 16;
-    bool found = false;
-    psrc = 0;
-    uint32_t p0 = 0;
-#pragma unroll
-    for (uint32_t s = 0; s < NSMAX; s++) {
-      const uint32_t rs = opaque(rem[s]);
-      const bool here = !found && pk < rs;
-      if (here) { psrc = s; p0 = opaque(pos[s]); found = true; }
-      else if (!found) pk -= rs;
-    }
-    pri = (((box0 + psrc) * P.M + p0) << 6) | x.lane;
-  };
-  if (total) {
-    pick(0, src, ri);
-    m = x.rec[ri];
-  }
-  while (total && !x.stop) {
-    const uint32_t type = hdr_type(m.x);
-    const uint32_t len = 1u + (type == PAXISIM_MSG_P1B ? hdr_n(m.x) : 0u);
-#pragma unroll
-    for (uint32_t s = 0; s < NSMAX; s++) {
-      const bool hit = s == src;
-      pos[s] = opaque(pos[s]) + (hit ? len : 0u);
-      rem[s] = opaque(rem[s]) - (hit ? len : 0u);
-    }
-    total -= len;
-    uint32_t nsrc = 0, nri = 0;
-    uint4 nm = make_uint4(0u, 0u, 0u, 0u);
-    if (total) {
-      pick(i + 1u, nsrc, nri);
-      nm = x.rec[nri];                                  // prefetch
-    }
-    if (src == N) {
-      x.client++;
-      handle_request<NT>(P, x, mkreq(m.w, PAXISIM_CLIENT_SRC));
-    } else {
-      switch (type) {                                   // node.handle dispatch (node.go:104-115)
-        case PAXISIM_MSG_REQUEST: x.dv[1]++; handle_request<NT>(P, x, mkreq(m.w, src)); break;
-        case PAXISIM_MSG_REPLY: x.dv[2]++; handle_reply<NT>(P, x, m.w); break;
-        case PAXISIM_MSG_P1A: x.dv[3]++; paxos_handle_p1a<NT>(P, x, m.y); break;
-        case PAXISIM_MSG_P1B: x.dv[4]++; paxos_handle_p1b<NT>(P, x, src, m.y, ri, hdr_n(m.x)); break;
-        case PAXISIM_MSG_P2A: x.dv[6]++; paxos_handle_p2a<NT>(P, x, m.y, (int32_t)m.z, m.w); break;
-        case PAXISIM_MSG_P2B: x.dv[7]++; paxos_handle_p2b<NT>(P, x, src, m.y, (int32_t)m.z); break;
-        case PAXISIM_MSG_P3: x.dv[8]++; paxos_handle_p3<NT>(P, x, m.y, (int32_t)m.z, m.w); break;
-        default: break;
-      }
-    }
-    src = nsrc;
-    ri = nri;
-    m = nm;
-    i++;
-  }
-#pragma unroll
-  for (uint32_t s = 0; s < NSMAX; s++)
-    if (s < NS) x.l_cnt[((box0 + s) << 6) | x.lane] = 0;
-  if (x.stop) atomicMin(&x.l_poison[x.lane], x.t);
-}
-
-// ---------------------------------------------------------------------------
-// The step kernel: workgroup = N waves (replicas) x 64 lanes (clusters)
-// ---------------------------------------------------------------------------
-template <int NT>
-__global__ void __launch_bounds__(NT ? NT * 64 : 1024) paxos_steps(Params P, uint32_t t0, uint32_t nsteps) {
-  extern __shared__ uint4 lds[];
-  const uint32_t N = nrep<NT>(P);
-  const uint32_t blk = blockIdx.x;
-  // stage the workgroup's HBM image into LDS
-  {
-    const uint4* g = reinterpret_cast<const uint4*>(P.image + (size_t)blk * P.img.bytes);
-    for (uint32_t k = threadIdx.x; k < P.img.bytes / 16u; k += blockDim.x) lds[k] = g[k];
-  }
-  uint8_t* L = reinterpret_cast<uint8_t*>(lds);
-  Rep<NT> x;
-  x.lane = threadIdx.x & 63u;
-  x.r = threadIdx.x >> 6;
-  x.blk = blk;
-  x.c = (uint64_t)blk * LANES + x.lane;
-  x.gid = P.cluster_base + x.c;
-  x.l_bal = reinterpret_cast<uint32_t*>(L + P.img.off_bal);
-  x.l_cmd = reinterpret_cast<uint32_t*>(L + P.img.off_cmd);
-  x.l_ack = reinterpret_cast<uint32_t*>(L + P.img.off_ack);
-  x.l_wcur = reinterpret_cast<uint32_t*>(L + P.img.off_wcur);
-  x.l_wiss = reinterpret_cast<uint32_t*>(L + P.img.off_wiss);
-  x.l_poison = reinterpret_cast<uint32_t*>(L + P.img.off_poison);
-  x.l_cnt = L + P.img.off_cnt;
-  x.rec = P.rec + (size_t)blk * P.rec_per_block;
-  const bool live = x.c < P.clusters && x.r < N;
-  if (live) {
+struct PaxosProto {
+  template <int NT>
+  __device__ static __forceinline__ void load(const Params& P, Rep<NT>& x) {
     const size_t i = rc(P, x.r, x.c);
-    x.kc = P.kc[x.c];
     x.ballot = P.ballot[i];
     x.slot = (int32_t)P.slot[i];
     x.execute = (int32_t)P.execute[i];
     const uint32_t meta = P.meta[i];
     x.active = meta & 1u;
     x.p1mask = meta >> 16;
-    x.flags = P.flags[i];
     x.npend = P.npend[i];
     x.nfwd = P.nfwd[i];
     x.digest = P.digest[i];
-#pragma unroll
-    for (uint32_t d = 0; d < Rep<NT>::NL; d++) {
-      x.du[d] = d < N ? P.link_drop[krc(P, d, x.r, x.c)] : 0u;
-      x.su[d] = d < N ? P.link_slow[krc(P, d, x.r, x.c)] : 0u;
-    }
   }
-#pragma unroll
-  for (int k = 0; k < 9; k++) x.dv[k] = 0;
-  x.client = x.sent = x.dropped = x.discarded = x.commits = x.replies = 0;
-  __syncthreads();
-
-  uint32_t b0 = t0 % P.D;
-  for (uint32_t t = t0; t < t0 + nsteps; t++) {
-    if (live && x.l_poison[x.lane] >= t) {
-      x.t = t;
-      x.b0 = b0;
-      paxos_replica_step<NT>(P, x);
-    }
-    if (++b0 == P.D) b0 = 0;
-    __syncthreads();
-  }
-
-  // write back: LDS image, registers, counters
-  {
-    uint4* g = reinterpret_cast<uint4*>(P.image + (size_t)blk * P.img.bytes);
-    for (uint32_t k = threadIdx.x; k < P.img.bytes / 16u; k += blockDim.x) g[k] = lds[k];
-  }
-  if (live) {
-    const uint32_t r = x.r;
-    const uint64_t c = x.c;
-    const size_t i = rc(P, r, c);
+  template <int NT>
+  __device__ static __forceinline__ void store(const Params& P, const Rep<NT>& x) {
+    const size_t i = rc(P, x.r, x.c);
     P.ballot[i] = x.ballot;
     P.slot[i] = (uint32_t)x.slot;
     P.execute[i] = (uint32_t)x.execute;
     P.meta[i] = (x.active & 1u) | (x.p1mask << 16);
-    P.flags[i] = x.flags;
     P.npend[i] = x.npend;
     P.nfwd[i] = x.nfwd;
     P.digest[i] = x.digest;
-#pragma unroll
-    for (uint32_t d = 0; d < Rep<NT>::NL; d++) {
-      if (d < N) {
-        P.link_drop[krc(P, d, r, c)] = x.du[d];
-        P.link_slow[krc(P, d, r, c)] = x.su[d];
-      }
-    }
-#pragma unroll
-    for (int k = 1; k < 9; k++)
-      if (x.dv[k]) P.stats[krc(P, ST_DELIV0 + k, r, c)] += x.dv[k];
-    P.stats[krc(P, ST_CLIENT, r, c)] += x.client;
-    P.stats[krc(P, ST_SENT, r, c)] += x.sent;
-    P.stats[krc(P, ST_DROPPED, r, c)] += x.dropped;
-    P.stats[krc(P, ST_DISCARDED, r, c)] += x.discarded;
-    P.stats[krc(P, ST_COMMITS, r, c)] += x.commits;
-    P.stats[krc(P, ST_REPLIES, r, c)] += x.replies;
   }
-}
+  template <int NT>
+  __device__ static __forceinline__ void client_request(const Params& P, Rep<NT>& x, uint32_t cid) {
+    handle_request<NT>(P, x, mkreq(cid, PAXISIM_CLIENT_SRC));
+  }
+  // node.handle dispatch (node.go:104-115; registrations paxos/replica.go:33-38)
+  template <int NT>
+  __device__ static __forceinline__ void dispatch(const Params& P, Rep<NT>& x, uint32_t src, const uint4& m,
+                                                  uint32_t ri) {
+    switch (hdr_type(m.x)) {
+      case PAXISIM_MSG_REQUEST: x.dv[PAXISIM_MSG_REQUEST]++; handle_request<NT>(P, x, mkreq(m.w, src)); break;
+      case PAXISIM_MSG_REPLY: x.dv[PAXISIM_MSG_REPLY]++; handle_reply<NT>(P, x, m.w); break;
+      case PAXISIM_MSG_P1A: x.dv[PAXISIM_MSG_P1A]++; paxos_handle_p1a<NT>(P, x, m.y); break;
+      case PAXISIM_MSG_P1B: x.dv[PAXISIM_MSG_P1B]++; paxos_handle_p1b<NT>(P, x, src, m.y, ri, hdr_n(m.x)); break;
+      case PAXISIM_MSG_P2A: x.dv[PAXISIM_MSG_P2A]++; paxos_handle_p2a<NT>(P, x, m.y, (int32_t)m.z, m.w); break;
+      case PAXISIM_MSG_P2B: x.dv[PAXISIM_MSG_P2B]++; paxos_handle_p2b<NT>(P, x, src, m.y, (int32_t)m.z); break;
+      case PAXISIM_MSG_P3: x.dv[PAXISIM_MSG_P3]++; paxos_handle_p3<NT>(P, x, m.y, (int32_t)m.z, m.w); break;
+      default: break;
+    }
+  }
+};
 
 }  // namespace pxs

@@ -1,0 +1,351 @@
+// sim_core.h — protocol-independent machinery of one replica-step on gfx950.
+//
+// A workgroup is N waves x 64 lanes: wave r plays replica r, lane l plays
+// cluster 64*blk + l.  This file holds what every protocol shares: the
+// replica's register state, the socket fault filter (socket.go:66-109), the
+// bucketed mailboxes, the PRNG-driven merge of per-source FIFO inboxes with
+// a one-message-ahead record prefetch, the closed-loop client
+// (benchmark.go:246-275) and the launch skeleton that stages the workgroup's
+// LDS image.  A protocol plugs in as a policy class with
+//   static void load(P, x) / store(P, x)        registers <-> HBM per launch
+//   static void dispatch(P, x, src, m, ri)      node.handle (node.go:104-115)
+//   static void client_request(P, x, cid)       the HTTP request path (http.go:99)
+#pragma once
+#include "paxisim_dev.h"
+
+namespace pxs {
+
+template <int NT>
+struct Rep {
+  static constexpr uint32_t NL = NT ? (uint32_t)NT : (uint32_t)PAXISIM_MAX_N;  // link registers
+  uint64_t c, gid;                      // global lane / cluster id
+  uint32_t lane, r, t, b0, hs, kc, blk;
+  // protocol registers (Paxos: ballot..digest; ABD: slot = op counter, execute = history length)
+  uint32_t ballot;
+  int32_t slot, execute;
+  uint32_t active, p1mask, flags, npend, nfwd;
+  uint64_t digest;
+  uint32_t du[NL], su[NL];              // link fault state: drop_until; slow_until | delay << 28
+  uint32_t dv[PAXISIM_NMSG];            // delivered by type (constant-indexed only)
+  uint32_t client, sent, dropped, discarded, commits, replies;
+  uint32_t send_seq;
+  bool stop, crashed;
+  // LDS views
+  uint32_t *l_a, *l_b, *l_c, *l_wcur, *l_wiss, *l_poison;
+  uint8_t* l_cnt;
+  uint4* rec;                           // this block's record region
+};
+
+template <int NT>
+__device__ __forceinline__ uint32_t nrep(const Params& P) { return NT ? (uint32_t)NT : P.N; }
+
+// The empty asm keeps LLVM from folding a select chain back into an alloca +
+// dynamic index (which would put the register array in scratch memory).
+__device__ __forceinline__ uint32_t opaque(uint32_t v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+template <int NT>
+__device__ __forceinline__ uint32_t lsel(const uint32_t (&a)[Rep<NT>::NL], uint32_t i) {
+  uint32_t v = opaque(a[0]);
+#pragma unroll
+  for (uint32_t k = 1; k < Rep<NT>::NL; k++) v = (i == k) ? opaque(a[k]) : v;
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// socket.Send (socket.go:66-109): crash -> drop -> flaky -> slow, then the
+// bounded (link, arrival-step) bucket.  Returns the record index to write.
+// ---------------------------------------------------------------------------
+template <int NT>
+__device__ __forceinline__ bool send_begin(const Params& P, Rep<NT>& x, uint32_t to, uint32_t nrec, uint32_t& ri) {
+  const uint32_t N = nrep<NT>(P);
+  const uint32_t seq = x.send_seq++;
+  x.sent++;
+  if (to >= N || x.crashed) { x.dropped++; return false; }
+  if (x.t < lsel<NT>(x.du, to) || (P.nfaults && scripted(P, PAXISIM_FAULT_DROP, x.gid, x.r, to, x.t, nullptr))) {
+    x.dropped++;
+    return false;
+  }
+  uint32_t delay = 0;
+  if (P.nfaults) {
+    uint32_t p = 0;
+    if (scripted(P, PAXISIM_FAULT_FLAKY, x.gid, x.r, to, x.t, &p) && p > 0 &&
+        ppm_hit(draw(x.hs, tag(PUR_FLAKY, x.r, seq)), p)) {
+      x.dropped++;
+      return false;
+    }
+  }
+  const uint32_t su = lsel<NT>(x.su, to);
+  if (x.t < (su & (T_MAX - 1u))) delay = su >> 28;
+  if (P.nfaults) scripted(P, PAXISIM_FAULT_SLOW, x.gid, x.r, to, x.t, &delay);
+  if (delay > P.max_delay) delay = P.max_delay;
+  uint32_t b = x.b0 + 1u + delay;
+  if (b >= P.D) b -= P.D;
+  const uint32_t box = (b * N + to) * P.NS + x.r;
+  uint8_t* cp = &x.l_cnt[(box << 6) | x.lane];
+  const uint32_t k = *cp;
+  if (k + nrec > P.M) {
+    x.flags |= PAXISIM_F_MBOX_OVF | PAXISIM_F_UNFAITHFUL;
+    x.dropped++;
+    return false;
+  }
+  *cp = (uint8_t)(k + nrec);
+  ri = ((box * P.M + k) << 6) | x.lane;
+  return true;
+}
+
+template <int NT>
+__device__ __forceinline__ void send1(const Params& P, Rep<NT>& x, uint32_t to, uint32_t w0, uint32_t w1,
+                                      uint32_t w2, uint32_t w3) {
+  uint32_t ri;
+  if (send_begin<NT>(P, x, to, 1, ri)) x.rec[ri] = make_uint4(w0, w1, w2, w3);
+}
+
+// Broadcast: every peer except self, IDs.Less order (socket.go:147-155; G1, G2)
+template <int NT>
+__device__ __forceinline__ void broadcast1(const Params& P, Rep<NT>& x, uint32_t w0, uint32_t w1, uint32_t w2,
+                                           uint32_t w3) {
+  const uint32_t N = nrep<NT>(P);
+#pragma nounroll
+  for (uint32_t d = 0; d < N; d++)
+    if (d != x.r) send1<NT>(P, x, d, w0, w1, w2, w3);
+}
+
+// ---------------------------------------------------------------------------
+// workload (benchmark.go:202-275): key and read/write of command cid
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wl_hash(uint32_t kc, uint32_t cid) { return fmix32(fmix32(kc ^ 0x5BD1E995u) ^ cid); }
+__device__ __forceinline__ uint32_t wl_key(const Params& P, uint32_t kc, uint32_t cid) { return wl_hash(kc, cid) % P.keys; }
+__device__ __forceinline__ bool wl_write(const Params& P, uint32_t kc, uint32_t cid) {
+  return ppm_hit(fmix32(wl_hash(kc, cid) ^ 0x27D4EB2Fu), P.write_ppm);
+}
+
+// The HTTP response reaches worker w, which issues its next request: it
+// arrives at the worker's target (client source N) in the next step.
+template <int NT>
+__device__ __forceinline__ void client_reply(const Params& P, Rep<NT>& x, uint32_t cid) {
+  const uint32_t w = (cid - 1u) % P.WK;
+  const uint32_t wi = (w << 6) | x.lane;
+  if (x.l_wcur[wi] != cid) return;              // duplicate reply: the worker moved on
+  x.replies++;
+  const uint32_t issued = x.l_wiss[wi];
+  if (P.max_requests == 0 || issued < P.max_requests) {
+    const uint64_t nc = 1ull + w + (uint64_t)P.WK * issued;
+    if (nc > CMD_MASK) {
+      x.flags |= PAXISIM_F_PEND_OVF | PAXISIM_F_UNFAITHFUL;
+      x.l_wcur[wi] = 0;
+      return;
+    }
+    x.l_wiss[wi] = issued + 1u;
+    x.l_wcur[wi] = (uint32_t)nc;
+    uint32_t b = x.b0 + 1u;
+    if (b >= P.D) b -= P.D;
+    const uint32_t box = (b * nrep<NT>(P) + P.target[w]) * P.NS + nrep<NT>(P);
+    uint8_t* cp = &x.l_cnt[(box << 6) | x.lane];
+    const uint32_t k = *cp;
+    if (k >= P.M) {
+      x.flags |= PAXISIM_F_MBOX_OVF | PAXISIM_F_UNFAITHFUL;
+      return;
+    }
+    x.rec[((box * P.M + k) << 6) | x.lane] = make_uint4(PAXISIM_MSG_REQUEST, 0u, 0u, (uint32_t)nc);
+    *cp = (uint8_t)(k + 1u);
+  } else {
+    x.l_wcur[wi] = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Random fault process: per idle outgoing link, one draw may open a drop and
+// / or a slow window.
+// ---------------------------------------------------------------------------
+template <int NT>
+__device__ __forceinline__ void fault_process(const Params& P, Rep<NT>& x) {
+  if (P.drop_ppm == 0 && P.slow_ppm == 0) return;
+#pragma unroll
+  for (uint32_t d = 0; d < Rep<NT>::NL; d++) {
+    if (d >= nrep<NT>(P) || d == x.r) continue;
+    const uint32_t u = draw(x.hs, tag(PUR_LINK, x.r, d));
+    if (P.drop_ppm && x.t >= x.du[d] && ppm_hit16(u & 0xFFFFu, P.drop_ppm)) x.du[d] = x.t + P.drop_len;
+    if (P.slow_ppm && x.t >= (x.su[d] & (T_MAX - 1u)) && ppm_hit16(u >> 16, P.slow_ppm)) {
+      const uint32_t span = P.slow_max - P.slow_min + 1u;
+      const uint32_t v = draw(x.hs, tag(PUR_SLOWD, x.r, d));
+      x.su[d] = (x.t + P.slow_len) | ((P.slow_min + __umulhi(v, span)) << 28);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// One replica, one step
+// ---------------------------------------------------------------------------
+template <int NT, class Proto>
+__device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x) {
+  constexpr uint32_t NSMAX = NT ? (uint32_t)NT + 1u : (uint32_t)PAXISIM_MAX_N + 1u;
+  const uint32_t N = nrep<NT>(P), NS = N + 1u;
+  x.send_seq = 0;
+  x.stop = false;
+  x.hs = step_key(x.kc, x.t);
+  fault_process<NT>(P, x);
+  x.crashed = P.nfaults && scripted(P, PAXISIM_FAULT_CRASH, x.gid, x.r, 0u, x.t, nullptr);
+
+  const uint32_t box0 = (x.b0 * N + x.r) * NS;          // inbox boxes: box0 + src
+  uint32_t rem[NSMAX], pos[NSMAX], total = 0;
+#pragma unroll
+  for (uint32_t s = 0; s < NSMAX; s++) {
+    rem[s] = 0;
+    pos[s] = 0;
+    if (s < NS) {
+      uint32_t n = x.l_cnt[((box0 + s) << 6) | x.lane];
+      if (x.crashed && s < N && n) {                    // socket.Recv discards (socket.go:111-118)
+        for (uint32_t k = 0; k < n;) {
+          const uint32_t h = x.rec[(((box0 + s) * P.M + k) << 6) | x.lane].x;
+          x.discarded++;
+          k += 1u + (hdr_type(h) == PAXISIM_MSG_P1B ? hdr_n(h) : 0u);
+        }
+        n = 0;
+      }
+      rem[s] = n;
+      total += n;
+    }
+  }
+
+  // merge order: weighted pick among sources, two 16-bit picks per draw;
+  // the next message's record is loaded before the current one is handled
+  uint32_t u = 0, i = 0, src = 0, ri = 0;
+  uint4 m = make_uint4(0u, 0u, 0u, 0u);
+  auto pick = [&](uint32_t idx, uint32_t& psrc, uint32_t& pri) {
+    if (!(idx & 1u)) u = draw(x.hs, tag(PUR_ORDER, x.r, idx >> 1));
+    uint32_t pk = (((idx & 1u) ? (u >> 16) : (u & 0xFFFFu)) * total) >> 16;
+    bool found = false;
+    psrc = 0;
+    uint32_t p0 = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < NSMAX; s++) {
+      const uint32_t rs = opaque(rem[s]);
+      const bool here = !found && pk < rs;
+      if (here) { psrc = s; p0 = opaque(pos[s]); found = true; }
+      else if (!found) pk -= rs;
+    }
+    pri = (((box0 + psrc) * P.M + p0) << 6) | x.lane;
+  };
+  if (total) {
+    pick(0, src, ri);
+    m = x.rec[ri];
+  }
+  while (total && !x.stop) {
+    const uint32_t type = hdr_type(m.x);
+    const uint32_t len = 1u + (type == PAXISIM_MSG_P1B ? hdr_n(m.x) : 0u);
+#pragma unroll
+    for (uint32_t s = 0; s < NSMAX; s++) {
+      const bool hit = s == src;
+      pos[s] = opaque(pos[s]) + (hit ? len : 0u);
+      rem[s] = opaque(rem[s]) - (hit ? len : 0u);
+    }
+    total -= len;
+    uint32_t nsrc = 0, nri = 0;
+    uint4 nm = make_uint4(0u, 0u, 0u, 0u);
+    if (total) {
+      pick(i + 1u, nsrc, nri);
+      nm = x.rec[nri];                                  // prefetch
+    }
+    if (src == N) {
+      x.client++;
+      Proto::template client_request<NT>(P, x, m.w);
+    } else {
+      Proto::template dispatch<NT>(P, x, src, m, ri);
+    }
+    src = nsrc;
+    ri = nri;
+    m = nm;
+    i++;
+  }
+#pragma unroll
+  for (uint32_t s = 0; s < NSMAX; s++)
+    if (s < NS) x.l_cnt[((box0 + s) << 6) | x.lane] = 0;
+  if (x.stop) atomicMin(&x.l_poison[x.lane], x.t);
+}
+
+// ---------------------------------------------------------------------------
+// The step kernel: stage the LDS image, run S steps, write everything back.
+// ---------------------------------------------------------------------------
+template <int NT, class Proto>
+__global__ void __launch_bounds__(NT ? NT * 64 : 1024) sim_steps(Params P, uint32_t t0, uint32_t nsteps) {
+  extern __shared__ uint4 lds[];
+  const uint32_t N = nrep<NT>(P);
+  const uint32_t blk = blockIdx.x;
+  {
+    const uint4* g = reinterpret_cast<const uint4*>(P.image + (size_t)blk * P.img.bytes);
+    for (uint32_t k = threadIdx.x; k < P.img.bytes / 16u; k += blockDim.x) lds[k] = g[k];
+  }
+  uint8_t* L = reinterpret_cast<uint8_t*>(lds);
+  Rep<NT> x;
+  x.lane = threadIdx.x & 63u;
+  x.r = threadIdx.x >> 6;
+  x.blk = blk;
+  x.c = (uint64_t)blk * LANES + x.lane;
+  x.gid = P.cluster_base + x.c;
+  x.l_a = reinterpret_cast<uint32_t*>(L + P.img.off_a);
+  x.l_b = reinterpret_cast<uint32_t*>(L + P.img.off_b);
+  x.l_c = reinterpret_cast<uint32_t*>(L + P.img.off_c);
+  x.l_wcur = reinterpret_cast<uint32_t*>(L + P.img.off_wcur);
+  x.l_wiss = reinterpret_cast<uint32_t*>(L + P.img.off_wiss);
+  x.l_poison = reinterpret_cast<uint32_t*>(L + P.img.off_poison);
+  x.l_cnt = L + P.img.off_cnt;
+  x.rec = P.rec + (size_t)blk * P.rec_per_block;
+  const bool live = x.c < P.clusters && x.r < N;
+  if (live) {
+    const size_t i = rc(P, x.r, x.c);
+    x.kc = P.kc[x.c];
+    x.flags = P.flags[i];
+#pragma unroll
+    for (uint32_t d = 0; d < Rep<NT>::NL; d++) {
+      x.du[d] = d < N ? P.link_drop[krc(P, d, x.r, x.c)] : 0u;
+      x.su[d] = d < N ? P.link_slow[krc(P, d, x.r, x.c)] : 0u;
+    }
+    Proto::template load<NT>(P, x);
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < PAXISIM_NMSG; k++) x.dv[k] = 0;
+  x.client = x.sent = x.dropped = x.discarded = x.commits = x.replies = 0;
+  __syncthreads();
+
+  uint32_t b0 = t0 % P.D;
+  for (uint32_t t = t0; t < t0 + nsteps; t++) {
+    if (live && x.l_poison[x.lane] >= t) {
+      x.t = t;
+      x.b0 = b0;
+      replica_step<NT, Proto>(P, x);
+    }
+    if (++b0 == P.D) b0 = 0;
+    __syncthreads();
+  }
+
+  {
+    uint4* g = reinterpret_cast<uint4*>(P.image + (size_t)blk * P.img.bytes);
+    for (uint32_t k = threadIdx.x; k < P.img.bytes / 16u; k += blockDim.x) g[k] = lds[k];
+  }
+  if (live) {
+    const uint32_t r = x.r;
+    const uint64_t c = x.c;
+    P.flags[rc(P, r, c)] = x.flags;
+#pragma unroll
+    for (uint32_t d = 0; d < Rep<NT>::NL; d++) {
+      if (d < N) {
+        P.link_drop[krc(P, d, r, c)] = x.du[d];
+        P.link_slow[krc(P, d, r, c)] = x.su[d];
+      }
+    }
+    Proto::template store<NT>(P, x);
+#pragma unroll
+    for (uint32_t k = 1; k < PAXISIM_NMSG; k++)
+      if (x.dv[k]) P.stats[krc(P, ST_DELIV0 + k, r, c)] += x.dv[k];
+    P.stats[krc(P, ST_CLIENT, r, c)] += x.client;
+    P.stats[krc(P, ST_SENT, r, c)] += x.sent;
+    P.stats[krc(P, ST_DROPPED, r, c)] += x.dropped;
+    P.stats[krc(P, ST_DISCARDED, r, c)] += x.discarded;
+    P.stats[krc(P, ST_COMMITS, r, c)] += x.commits;
+    P.stats[krc(P, ST_REPLIES, r, c)] += x.replies;
+  }
+}
+
+}  // namespace pxs

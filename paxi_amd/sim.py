@@ -37,6 +37,12 @@ def load_library():
     L.paxisim_sync.argtypes = [C.c_void_p]
     L.paxisim_kernel_time.restype = C.c_int
     L.paxisim_kernel_time.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.c_int]
+    L.paxisim_linearizable.restype = C.c_int
+    L.paxisim_linearizable.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                       C.POINTER(C.c_uint64)]
+    L.paxisim_history.restype = C.c_int
+    L.paxisim_history.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32), C.c_uint32,
+                                  C.POINTER(C.c_uint32)]
     L.paxisim_device_bytes.restype = C.c_int
     L.paxisim_device_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     if L.paxisim_abi_version() != abi.ABI_VERSION:
@@ -47,7 +53,8 @@ def load_library():
 
 EXPORTED = ["paxisim_abi_version", "paxisim_last_error", "paxisim_create", "paxisim_destroy",
             "paxisim_fault_add", "paxisim_step", "paxisim_sync", "paxisim_stats_get",
-            "paxisim_read_state", "paxisim_check", "paxisim_kernel_time", "paxisim_device_bytes"]
+            "paxisim_read_state", "paxisim_check", "paxisim_kernel_time", "paxisim_device_bytes",
+            "paxisim_linearizable", "paxisim_history"]
 
 
 def _check(rc):
@@ -92,6 +99,19 @@ class Simulation:
         v = C.c_uint64()
         _check(load_library().paxisim_check(self.h, C.byref(v)))
         return v.value
+
+    def linearizable(self):
+        """History.Linearizable (history.go:55-71): (anomalies, ops checked, partitions skipped)."""
+        a, n, sk = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        _check(load_library().paxisim_linearizable(self.h, C.byref(a), C.byref(n), C.byref(sk)))
+        return a.value, n.value, sk.value
+
+    def history(self, cluster):
+        n = C.c_uint32()
+        _check(load_library().paxisim_history(self.h, cluster, None, 0, C.byref(n)))
+        buf = (C.c_uint32 * max(1, 5 * n.value))()
+        _check(load_library().paxisim_history(self.h, cluster, buf, n.value, C.byref(n)))
+        return [tuple(buf[5 * i: 5 * i + 5]) for i in range(n.value)]
 
     def kernel_time(self, reset=False):
         ms, n = C.c_double(), C.c_uint64()

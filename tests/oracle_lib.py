@@ -25,6 +25,11 @@ def lib():
         L.oracle_exec_log.restype = C.c_int
         L.oracle_exec_log.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.POINTER(C.c_uint32),
                                       C.c_uint32, C.POINTER(C.c_uint32)]
+        L.oracle_lin_check.restype = C.c_int
+        L.oracle_lin_check.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.oracle_history.restype = C.c_int
+        L.oracle_history.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32), C.c_uint32,
+                                     C.POINTER(C.c_uint32)]
         L.oracle_new_ballot.restype = C.c_uint64
         L.oracle_new_ballot.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
         L.oracle_ballot_next.restype = C.c_uint64
@@ -78,6 +83,18 @@ class OracleSim:
         buf = (C.c_uint32 * max(1, n.value))()
         _check(lib().oracle_exec_log(self.h, cluster, replica, buf, n.value, C.byref(n)))
         return list(buf[: n.value])
+
+    def linearizable(self):
+        a, n = C.c_uint64(), C.c_uint64()
+        _check(lib().oracle_lin_check(self.h, C.byref(a), C.byref(n)))
+        return a.value, n.value
+
+    def history(self, cluster):
+        n = C.c_uint32()
+        _check(lib().oracle_history(self.h, cluster, None, 0, C.byref(n)))
+        buf = (C.c_uint32 * max(1, 5 * n.value))()
+        _check(lib().oracle_history(self.h, cluster, buf, n.value, C.byref(n)))
+        return [tuple(buf[5 * i: 5 * i + 5]) for i in range(n.value)]
 
     def close(self):
         if self.h:
