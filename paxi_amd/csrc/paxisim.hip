@@ -68,7 +68,8 @@ __global__ void init_kernel(Params P) {
   uint8_t* img = P.image + (size_t)blk * P.img.bytes;
   P.kc[c] = cluster_key(P.seed, P.cluster_base + c);
   reinterpret_cast<uint32_t*>(img + P.img.off_poison)[lane] = 0xFFFFFFFFu;
-  for (uint32_t r = 0; r < P.N; r++) P.slot[rc(P, r, c)] = 0xFFFFFFFFu;   // slot: -1 (paxos.go:45)
+  if (P.protocol == PAXISIM_PAXOS)
+    for (uint32_t r = 0; r < P.N; r++) P.slot[rc(P, r, c)] = 0xFFFFFFFFu;   // slot: -1 (paxos.go:45)
   if (c >= P.clusters) return;
   uint8_t* cnt = img + P.img.off_cnt;
   uint32_t* wcur = reinterpret_cast<uint32_t*>(img + P.img.off_wcur);
@@ -293,6 +294,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
   P.D = cfg->max_delay + 2u;
   P.NS = N + 1u;
   P.WK = wl->outstanding;
+  P.wk_magic = 0xFFFFFFFFu / P.WK;
   P.max_requests = wl->max_requests;
   P.clusters = cfg->clusters;
   P.C = (cfg->clusters + LANES - 1) / LANES * LANES;

@@ -78,6 +78,7 @@ enum { ABD_FREE = 0, ABD_GET = 1, ABD_SET = 2, ABD_DONE = 3 };
 struct Params {
   uint32_t protocol, N, Z, W, M, D, NS, WK, max_requests;
   uint32_t keys, write_ppm, H, OW;
+  uint32_t wk_magic;     // floor((2^32-1)/WK): (x % WK) by multiply-high + one correction
   uint64_t C;            // allocated cluster lanes (multiple of 64)
   uint64_t clusters;     // live clusters
   uint64_t cluster_base, seed;

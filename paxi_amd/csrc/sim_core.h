@@ -29,6 +29,8 @@ struct Rep {
   uint32_t dv[PAXISIM_NMSG];            // delivered by type (constant-indexed only)
   uint32_t client, sent, dropped, discarded, commits, replies;
   uint32_t send_seq;
+  uint32_t dmask, fmask;                // per-step: dropped / flaky destinations
+  uint64_t dly;                         // per-step: 4-bit delay per destination
   bool stop, crashed;
   // LDS views
   uint32_t *l_a, *l_b, *l_c, *l_wcur, *l_wiss, *l_poison;
@@ -59,30 +61,18 @@ __device__ __forceinline__ uint32_t lsel(const uint32_t (&a)[Rep<NT>::NL], uint3
 // ---------------------------------------------------------------------------
 template <int NT>
 __device__ __forceinline__ bool send_begin(const Params& P, Rep<NT>& x, uint32_t to, uint32_t nrec, uint32_t& ri) {
-  const uint32_t N = nrep<NT>(P);
   const uint32_t seq = x.send_seq++;
   x.sent++;
-  if (to >= N || x.crashed) { x.dropped++; return false; }
-  if (x.t < lsel<NT>(x.du, to) || (P.nfaults && scripted(P, PAXISIM_FAULT_DROP, x.gid, x.r, to, x.t, nullptr))) {
-    x.dropped++;
-    return false;
-  }
-  uint32_t delay = 0;
-  if (P.nfaults) {
+  // crash, unknown id (socket.go:86-88) and drop were folded into dmask at step start
+  if (to >= nrep<NT>(P) || ((x.dmask >> to) & 1u)) { x.dropped++; return false; }
+  if ((x.fmask >> to) & 1u) {                          // flaky (socket.go:77-81), scripted only
     uint32_t p = 0;
-    if (scripted(P, PAXISIM_FAULT_FLAKY, x.gid, x.r, to, x.t, &p) && p > 0 &&
-        ppm_hit(draw(x.hs, tag(PUR_FLAKY, x.r, seq)), p)) {
-      x.dropped++;
-      return false;
-    }
+    scripted(P, PAXISIM_FAULT_FLAKY, x.gid, x.r, to, x.t, &p);
+    if (ppm_hit(draw(x.hs, tag(PUR_FLAKY, x.r, seq)), p)) { x.dropped++; return false; }
   }
-  const uint32_t su = lsel<NT>(x.su, to);
-  if (x.t < (su & (T_MAX - 1u))) delay = su >> 28;
-  if (P.nfaults) scripted(P, PAXISIM_FAULT_SLOW, x.gid, x.r, to, x.t, &delay);
-  if (delay > P.max_delay) delay = P.max_delay;
-  uint32_t b = x.b0 + 1u + delay;
+  uint32_t b = x.b0 + 1u + (uint32_t)((x.dly >> (4u * to)) & 15u);   // slow (socket.go:99-106)
   if (b >= P.D) b -= P.D;
-  const uint32_t box = (b * N + to) * P.NS + x.r;
+  const uint32_t box = (b * nrep<NT>(P) + to) * P.NS + x.r;
   uint8_t* cp = &x.l_cnt[(box << 6) | x.lane];
   const uint32_t k = *cp;
   if (k + nrec > P.M) {
@@ -93,6 +83,34 @@ __device__ __forceinline__ bool send_begin(const Params& P, Rep<NT>& x, uint32_t
   *cp = (uint8_t)(k + nrec);
   ri = ((box * P.M + k) << 6) | x.lane;
   return true;
+}
+
+// Per step: fold crash / drop / slow / flaky of every outgoing link into masks
+// (the filter order crash -> drop -> flaky -> slow is kept by send_begin).
+template <int NT>
+__device__ __forceinline__ void link_masks(const Params& P, Rep<NT>& x) {
+  const uint32_t N = nrep<NT>(P);
+  uint32_t dm = 0, fm = 0;
+  uint64_t dl = 0;
+#pragma unroll
+  for (uint32_t d = 0; d < Rep<NT>::NL; d++) {
+    if (d >= N) continue;
+    uint32_t delay = 0;
+    bool drop = x.t < x.du[d];
+    if (x.t < (x.su[d] & (T_MAX - 1u))) delay = x.su[d] >> 28;
+    if (P.nfaults) {
+      drop = drop || scripted(P, PAXISIM_FAULT_DROP, x.gid, x.r, d, x.t, nullptr);
+      uint32_t p = 0;
+      if (scripted(P, PAXISIM_FAULT_FLAKY, x.gid, x.r, d, x.t, &p) && p > 0) fm |= 1u << d;
+      scripted(P, PAXISIM_FAULT_SLOW, x.gid, x.r, d, x.t, &delay);
+    }
+    if (delay > P.max_delay) delay = P.max_delay;
+    dm |= (drop || x.crashed) ? (1u << d) : 0u;
+    dl |= (uint64_t)delay << (4u * d);
+  }
+  x.dmask = dm;
+  x.fmask = fm;
+  x.dly = dl;
 }
 
 template <int NT>
@@ -106,10 +124,10 @@ __device__ __forceinline__ void send1(const Params& P, Rep<NT>& x, uint32_t to, 
 template <int NT>
 __device__ __forceinline__ void broadcast1(const Params& P, Rep<NT>& x, uint32_t w0, uint32_t w1, uint32_t w2,
                                            uint32_t w3) {
-  const uint32_t N = nrep<NT>(P);
-#pragma nounroll
-  for (uint32_t d = 0; d < N; d++)
-    if (d != x.r) send1<NT>(P, x, d, w0, w1, w2, w3);
+  constexpr uint32_t NU = NT ? (uint32_t)NT : (uint32_t)PAXISIM_MAX_N;
+#pragma unroll
+  for (uint32_t d = 0; d < NU; d++)
+    if (d < nrep<NT>(P) && d != x.r) send1<NT>(P, x, d, w0, w1, w2, w3);
 }
 
 // ---------------------------------------------------------------------------
@@ -125,7 +143,8 @@ __device__ __forceinline__ bool wl_write(const Params& P, uint32_t kc, uint32_t 
 // arrives at the worker's target (client source N) in the next step.
 template <int NT>
 __device__ __forceinline__ void client_reply(const Params& P, Rep<NT>& x, uint32_t cid) {
-  const uint32_t w = (cid - 1u) % P.WK;
+  uint32_t w = (cid - 1u) - P.WK * __umulhi(cid - 1u, P.wk_magic);   // (cid-1) % WK
+  if (w >= P.WK) w -= P.WK;
   const uint32_t wi = (w << 6) | x.lane;
   if (x.l_wcur[wi] != cid) return;              // duplicate reply: the worker moved on
   x.replies++;
@@ -187,6 +206,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x) {
   x.hs = step_key(x.kc, x.t);
   fault_process<NT>(P, x);
   x.crashed = P.nfaults && scripted(P, PAXISIM_FAULT_CRASH, x.gid, x.r, 0u, x.t, nullptr);
+  link_masks<NT>(P, x);
 
   const uint32_t box0 = (x.b0 * N + x.r) * NS;          // inbox boxes: box0 + src
   uint32_t rem[NSMAX], pos[NSMAX], total = 0;

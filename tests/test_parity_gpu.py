@@ -53,7 +53,7 @@ def test_config1_kats_on_gpu():
 
 @pytest.mark.parametrize("npz", [[3], [5], [3, 3, 3], [2, 2], [7]])
 def test_faults_random_process(npz):
-    cfg = abi.make_config(npz=npz, clusters=300, seed=42, window=32, mbox_cap=16, max_delay=4)
+    cfg = abi.make_config(npz=npz, clusters=300, seed=42, window=16, mbox_cap=16, max_delay=4)
     wl = abi.make_workload(outstanding=8, target=0)
     fp = abi.make_fault_process(drop_ppm=3000, drop_len=25, slow_ppm=3000, slow_len=25, slow_min=1, slow_max=4)
     g, o = run_both(cfg, wl, fp, steps=400)
@@ -144,3 +144,19 @@ def test_single_cluster_and_ragged_tail():
         wl = abi.make_workload(outstanding=3, target=0)
         g, o = run_both(cfg, wl, steps=120)
         assert_same(g, o, f"C={n}")
+
+
+def test_oversized_workgroup_image_is_refused():
+    """N=9 with a 64-slot window needs more than 160 KB of LDS: EUNSUPP, not a crash."""
+    from paxi_amd.sim import PaxisimError
+    with pytest.raises(PaxisimError, match="exceeds LDS"):
+        _sim()(abi.make_config(npz=[3, 3, 3], clusters=64, window=64), abi.make_workload())
+
+
+def test_window32_n5():
+    """W=32 still fits at N=5 (one workgroup per CU)."""
+    cfg = abi.make_config(npz=[5], clusters=200, seed=4, window=32)
+    wl = abi.make_workload(outstanding=8, target=0)
+    fp = abi.make_fault_process(drop_ppm=3000, drop_len=25, slow_ppm=3000, slow_len=25, slow_min=1, slow_max=4)
+    g, o = run_both(cfg, wl, fp, steps=300)
+    assert_same(g, o, "W=32")
