@@ -53,14 +53,14 @@ __device__ __forceinline__ void abd_handle_request(const Params& P, Rep<NT>& x, 
   x.l_c[op_i<NT>(P, x, opid, 3)] = x.l_a[ki];
   x.l_c[op_i<NT>(P, x, opid, 4)] = x.l_b[ki];
   x.l_c[op_i<NT>(P, x, opid, 5)] = x.t;
-  broadcast1<NT>(P, x, PAXISIM_MSG_GET | (k << 8), opid, 0u, 0u);
+  post_broadcast<NT>(P, x, PAXISIM_MSG_GET | (k << 8), opid, 0u, 0u);
 }
 
 template <int NT>
 __device__ __forceinline__ void abd_handle_get(const Params& P, Rep<NT>& x, uint32_t src, uint32_t key,
                                                uint32_t opid) {                     // replica.go:73-82
   const uint32_t ki = kv_i<NT>(P, x, key);
-  send1<NT>(P, x, src, PAXISIM_MSG_GETREPLY | (key << 8), opid, x.l_b[ki], x.l_a[ki]);
+  post_unicast<NT>(P, x, src, PAXISIM_MSG_GETREPLY | (key << 8), opid, x.l_b[ki], x.l_a[ki]);
 }
 
 template <int NT>
@@ -71,7 +71,7 @@ __device__ __forceinline__ void abd_handle_set(const Params& P, Rep<NT>& x, uint
     abd_put<NT>(P, x, key, val);
     x.l_b[ki] = ver;
   }
-  send1<NT>(P, x, src, PAXISIM_MSG_SETREPLY | (key << 8), opid, 0u, 0u);
+  post_unicast<NT>(P, x, src, PAXISIM_MSG_SETREPLY | (key << 8), opid, 0u, 0u);
 }
 
 template <int NT>
@@ -100,7 +100,7 @@ __device__ __forceinline__ void abd_handle_getreply(const Params& P, Rep<NT>& x,
       abd_put<NT>(P, x, key, ev);
       x.l_b[ki] = en;
     }
-    broadcast1<NT>(P, x, PAXISIM_MSG_SET | (key << 8), opid, en, ev);
+    post_broadcast<NT>(P, x, PAXISIM_MSG_SET | (key << 8), opid, en, ev);
   }
   x.l_c[si] = sm;
   x.l_c[vi] = ev;

@@ -618,3 +618,22 @@ extern "C" int paxisim_linearizable(paxisim* h, uint64_t* anomalies, uint64_t* o
   if (skipped) *skipped = res[2];
   return 0;
 }
+
+#ifdef PXS_STAMPS
+// Diagnostic build only: per (block, replica) {setup, loop, barrier cycles, loop trips, records, steps}.
+extern "C" int paxisim_dbg_enable(paxisim* h) {
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const size_t n = (h->P.C / LANES) * 16 * 16;
+  HIPCHK(hipMalloc(&h->P.dbg, n * 8));
+  HIPCHK(hipMemset(h->P.dbg, 0, n * 8));
+  return 0;
+}
+extern "C" int paxisim_dbg_read(paxisim* h, unsigned long long* out) {
+  HIPCHK(hipSetDevice(h->cfg.device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  const size_t n = (h->P.C / LANES) * 16 * 16;
+  HIPCHK(hipMemcpy(out, h->P.dbg, n * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemset(h->P.dbg, 0, n * 8));
+  return 0;
+}
+#endif

@@ -102,6 +102,7 @@ struct Params {
   uint32_t* reqx;        // [blk][N][W][64] request side table (Paxos)
   uint4* hist;           // [N][C][H] completed ABD ops {key|write<<31, value, start, end}
   uint8_t* image;        // [blk][img.bytes]
+  unsigned long long* dbg;  // diagnostic build only (PXS_STAMPS): per-wave phase totals
   uint4* rec;            // [blk][D][dst][src][M][64]
 };
 

@@ -67,7 +67,7 @@ template <int NT>
 __device__ __forceinline__ void request_reply(const Params& P, Rep<NT>& x, uint32_t req, uint32_t reply_cmd) {
   const uint32_t o = req_origin(req);
   if (o == PAXISIM_CLIENT_SRC) client_reply<NT>(P, x, req_cid(req));
-  else send1<NT>(P, x, o, PAXISIM_MSG_REPLY, 0u, 0u, reply_cmd);
+  else post_unicast<NT>(P, x, o, PAXISIM_MSG_REPLY, 0u, 0u, reply_cmd);
 }
 
 // node.Forward (node.go:165-172)
@@ -83,7 +83,7 @@ __device__ __forceinline__ void node_forward(const Params& P, Rep<NT>& x, uint32
   } else {
     P.fwd[krc(P, i, x.r, x.c)] = req;
   }
-  send1<NT>(P, x, to, PAXISIM_MSG_REQUEST, 0u, 0u, cid);
+  post_unicast<NT>(P, x, to, PAXISIM_MSG_REQUEST, 0u, 0u, cid);
 }
 
 // node.recv Reply case (node.go:83-90)
@@ -122,7 +122,7 @@ __device__ __forceinline__ void paxos_p1a(const Params& P, Rep<NT>& x) {      //
   if ((x.ballot >> 4) + 1u >= (1u << 27)) x.flags |= PAXISIM_F_BALLOT_OVF | PAXISIM_F_UNFAITHFUL;
   x.ballot = bal_next(x.ballot, x.r);
   x.p1mask = 1u << x.r;
-  broadcast1<NT>(P, x, PAXISIM_MSG_P1A, x.ballot, 0u, 0u);
+  post_broadcast<NT>(P, x, PAXISIM_MSG_P1A, x.ballot, 0u, 0u);
 }
 
 template <int NT>
@@ -136,14 +136,15 @@ __device__ __forceinline__ void paxos_p2a(const Params& P, Rep<NT>& x, uint32_t 
   } else {
     x.flags |= PAXISIM_F_WOVF | PAXISIM_F_UNFAITHFUL;
   }
-  if (P.thrifty) {                                   // MulticastQuorum(N/2+1) (socket.go:132-145)
+  if (P.thrifty) {                                   // MulticastQuorum(N/2+1) (socket.go:132-145), ring order
     const uint32_t N = nrep<NT>(P);
     uint32_t sent = 0;
+    intent_flush<NT>(P, x);
 #pragma nounroll
     for (uint32_t i = 1; i < N && sent < N / 2 + 1; i++, sent++)
       send1<NT>(P, x, (x.r + i) % N, PAXISIM_MSG_P2A, x.ballot, (uint32_t)x.slot, cid);
   } else {
-    broadcast1<NT>(P, x, PAXISIM_MSG_P2A, x.ballot, (uint32_t)x.slot, cid);
+    post_broadcast<NT>(P, x, PAXISIM_MSG_P2A, x.ballot, (uint32_t)x.slot, cid);
   }
 }
 
@@ -201,6 +202,7 @@ __device__ __forceinline__ void paxos_handle_p1a(const Params& P, Rep<NT>& x, ui
     n += (c & EF_EXISTS) && !(c & EF_COMMIT);
   }
   uint32_t ri;
+  intent_flush<NT>(P, x);                                                    // keep per-link order
   if (!send_begin<NT>(P, x, bal_id(mb), 1u + n, ri)) return;
   x.rec[ri] = make_uint4(PAXISIM_MSG_P1B | (n << 8), x.ballot, 0u, 0u);
   for (int32_t s = x.execute; s <= hi; s++) {
@@ -257,7 +259,7 @@ __device__ __forceinline__ void paxos_handle_p1b(const Params& P, Rep<NT>& x, ui
         x.l_a[i] = x.ballot;
         x.l_b[i] = c | EF_QUORUM;
         x.l_c[i] = 1u << x.r;
-        broadcast1<NT>(P, x, PAXISIM_MSG_P2A, x.ballot, (uint32_t)s, c & CMD_MASK);
+        post_broadcast<NT>(P, x, PAXISIM_MSG_P2A, x.ballot, (uint32_t)s, c & CMD_MASK);
       }
       const uint32_t np = x.npend;
       x.npend = 0;
@@ -296,7 +298,7 @@ __device__ __forceinline__ void paxos_handle_p2a(const Params& P, Rep<NT>& x, ui
       x.flags |= PAXISIM_F_WOVF;
     }
   }
-  send1<NT>(P, x, bal_id(mb), PAXISIM_MSG_P2B, x.ballot, (uint32_t)ms, 0u);
+  post_unicast<NT>(P, x, bal_id(mb), PAXISIM_MSG_P2B, x.ballot, (uint32_t)ms, 0u);
 }
 
 template <int NT>
@@ -326,7 +328,7 @@ __device__ __forceinline__ void paxos_handle_p2b(const Params& P, Rep<NT>& x, ui
     if (quorum_ok(P, P.q2, ack)) {
       x.l_b[i] = c | EF_COMMIT;
       x.commits++;
-      broadcast1<NT>(P, x, PAXISIM_MSG_P3, mb, (uint32_t)ms, c & CMD_MASK);
+      post_broadcast<NT>(P, x, PAXISIM_MSG_P3, mb, (uint32_t)ms, c & CMD_MASK);
       if (P.rwc) {
         const uint32_t q = ereq<NT>(P, x, i, c);
         if (!q) { x.flags |= PAXISIM_F_POISON; x.stop = true; return; }   // nil r.Reply

@@ -30,6 +30,8 @@ struct Rep {
   uint32_t client, sent, dropped, discarded, commits, replies;
   uint32_t send_seq;
   uint32_t dmask, fmask;                // per-step: dropped / flaky destinations
+  uint32_t im;                          // pending send intent: destination mask (0 = none)
+  uint32_t iw0, iw1, iw2, iw3;          // pending send intent: the record
   uint64_t dly;                         // per-step: 4-bit delay per destination
   bool stop, crashed;
   // LDS views
@@ -131,6 +133,48 @@ __device__ __forceinline__ void broadcast1(const Params& P, Rep<NT>& x, uint32_t
 }
 
 // ---------------------------------------------------------------------------
+// Send intents.  A handler posts at most one pending send (one record to a set
+// of destinations); the merge loop emits it after the dispatch switch, so the
+// socket-filter / mailbox code runs once per iteration for all lanes instead of
+// once per handler branch.  Posting a second send first emits the pending one,
+// and emission walks destinations in index order, so every link sees its
+// records in exactly the order the handlers issued them.
+// ---------------------------------------------------------------------------
+template <int NT>
+__device__ __forceinline__ void intent_flush(const Params& P, Rep<NT>& x) {
+  if (!x.im) return;
+  constexpr uint32_t NU = NT ? (uint32_t)NT : (uint32_t)PAXISIM_MAX_N;
+#pragma unroll
+  for (uint32_t d = 0; d < NU; d++)
+    if (d < nrep<NT>(P) && ((x.im >> d) & 1u)) send1<NT>(P, x, d, x.iw0, x.iw1, x.iw2, x.iw3);
+  x.im = 0;
+}
+template <int NT>
+__device__ __forceinline__ void post_mask(const Params& P, Rep<NT>& x, uint32_t mask, uint32_t w0, uint32_t w1,
+                                          uint32_t w2, uint32_t w3) {
+  intent_flush<NT>(P, x);
+  x.im = mask;
+  x.iw0 = w0; x.iw1 = w1; x.iw2 = w2; x.iw3 = w3;
+}
+// Send(to, m) (socket.go:66)
+template <int NT>
+__device__ __forceinline__ void post_unicast(const Params& P, Rep<NT>& x, uint32_t to, uint32_t w0, uint32_t w1,
+                                             uint32_t w2, uint32_t w3) {
+  if (to >= nrep<NT>(P)) {                // unknown id ("0.0"): counted and dropped in order
+    intent_flush<NT>(P, x);
+    send1<NT>(P, x, to, w0, w1, w2, w3);
+    return;
+  }
+  post_mask<NT>(P, x, 1u << to, w0, w1, w2, w3);
+}
+// Broadcast(m) (socket.go:147-155)
+template <int NT>
+__device__ __forceinline__ void post_broadcast(const Params& P, Rep<NT>& x, uint32_t w0, uint32_t w1, uint32_t w2,
+                                               uint32_t w3) {
+  post_mask<NT>(P, x, ((1u << nrep<NT>(P)) - 1u) & ~(1u << x.r), w0, w1, w2, w3);
+}
+
+// ---------------------------------------------------------------------------
 // workload (benchmark.go:202-275): key and read/write of command cid
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t wl_hash(uint32_t kc, uint32_t cid) { return fmix32(fmix32(kc ^ 0x5BD1E995u) ^ cid); }
@@ -197,12 +241,30 @@ __device__ __forceinline__ void fault_process(const Params& P, Rep<NT>& x) {
 // ---------------------------------------------------------------------------
 // One replica, one step
 // ---------------------------------------------------------------------------
+#ifdef PXS_STAMPS
+struct Stamps { unsigned long long setup, loop, barrier, trips, msgs, steps, pick, disp, wait, flush; };
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+#endif
+
 template <int NT, class Proto>
-__device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x) {
+__device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
+#ifdef PXS_STAMPS
+                                             , void* stp
+#endif
+) {
+#ifdef PXS_STAMPS
+  Stamps& st = *reinterpret_cast<Stamps*>(stp);
+  const unsigned long long s0 = stamp();
+#endif
   constexpr uint32_t NSMAX = NT ? (uint32_t)NT + 1u : (uint32_t)PAXISIM_MAX_N + 1u;
   const uint32_t N = nrep<NT>(P), NS = N + 1u;
   x.send_seq = 0;
   x.stop = false;
+  x.im = 0;
   x.hs = step_key(x.kc, x.t);
   fault_process<NT>(P, x);
   x.crashed = P.nfaults && scripted(P, PAXISIM_FAULT_CRASH, x.gid, x.r, 0u, x.t, nullptr);
@@ -231,6 +293,15 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x) {
 
   // merge order: weighted pick among sources, two 16-bit picks per draw;
   // the next message's record is loaded before the current one is handled
+#ifdef PXS_STAMPS
+  const unsigned long long s1 = stamp();
+  st.setup += s1 - s0;
+  {
+    uint32_t tot = total;
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+    st.msgs += tot;   // records (~messages) over the wave's lanes
+  }
+#endif
   uint32_t u = 0, i = 0, src = 0, ri = 0;
   uint4 m = make_uint4(0u, 0u, 0u, 0u);
   auto pick = [&](uint32_t idx, uint32_t& psrc, uint32_t& pri) {
@@ -253,6 +324,12 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x) {
     m = x.rec[ri];
   }
   while (total && !x.stop) {
+#ifdef PXS_STAMPS
+    const unsigned long long w0 = stamp();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long w1 = stamp();
+    st.wait += w1 - w0;
+#endif
     const uint32_t type = hdr_type(m.x);
     const uint32_t len = 1u + (type == PAXISIM_MSG_P1B ? hdr_n(m.x) : 0u);
 #pragma unroll
@@ -262,18 +339,36 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x) {
       rem[s] = opaque(rem[s]) - (hit ? len : 0u);
     }
     total -= len;
+#ifdef PXS_STAMPS
+    const unsigned long long q0 = stamp();
+#endif
     uint32_t nsrc = 0, nri = 0;
     uint4 nm = make_uint4(0u, 0u, 0u, 0u);
     if (total) {
       pick(i + 1u, nsrc, nri);
       nm = x.rec[nri];                                  // prefetch
     }
+#ifdef PXS_STAMPS
+    const unsigned long long q1 = stamp();
+    st.pick += q1 - q0;
+#endif
     if (src == N) {
       x.client++;
       Proto::template client_request<NT>(P, x, m.w);
     } else {
       Proto::template dispatch<NT>(P, x, src, m, ri);
     }
+#ifdef PXS_STAMPS
+    const unsigned long long q2 = stamp();
+    st.disp += q2 - q1;
+#endif
+    intent_flush<NT>(P, x);                             // one emit point for all lanes
+#ifdef PXS_STAMPS
+    st.flush += stamp() - q2;
+#endif
+#ifdef PXS_STAMPS
+    st.trips += 1;
+#endif
     src = nsrc;
     ri = nri;
     m = nm;
@@ -283,13 +378,16 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x) {
   for (uint32_t s = 0; s < NSMAX; s++)
     if (s < NS) x.l_cnt[((box0 + s) << 6) | x.lane] = 0;
   if (x.stop) atomicMin(&x.l_poison[x.lane], x.t);
+#ifdef PXS_STAMPS
+  st.loop += stamp() - s1;
+#endif
 }
 
 // ---------------------------------------------------------------------------
 // The step kernel: stage the LDS image, run S steps, write everything back.
 // ---------------------------------------------------------------------------
 template <int NT, class Proto>
-__global__ void __launch_bounds__(NT ? NT * 64 : 1024) sim_steps(Params P, uint32_t t0, uint32_t nsteps) {
+__global__ void __launch_bounds__(NT ? NT * 64 : 1024, 3) sim_steps(Params P, uint32_t t0, uint32_t nsteps) {
   extern __shared__ uint4 lds[];
   const uint32_t N = nrep<NT>(P);
   const uint32_t blk = blockIdx.x;
@@ -300,7 +398,10 @@ __global__ void __launch_bounds__(NT ? NT * 64 : 1024) sim_steps(Params P, uint3
   uint8_t* L = reinterpret_cast<uint8_t*>(lds);
   Rep<NT> x;
   x.lane = threadIdx.x & 63u;
-  x.r = threadIdx.x >> 6;
+  // replica played by this wave, rotated per workgroup: the busiest replica
+  // (the leader) then sits on a different wave -> SIMD in neighbouring workgroups
+  x.r = (threadIdx.x >> 6) + blk % N;
+  if (x.r >= N) x.r -= N;
   x.blk = blk;
   x.c = (uint64_t)blk * LANES + x.lane;
   x.gid = P.cluster_base + x.c;
@@ -330,15 +431,38 @@ __global__ void __launch_bounds__(NT ? NT * 64 : 1024) sim_steps(Params P, uint3
   __syncthreads();
 
   uint32_t b0 = t0 % P.D;
+#ifdef PXS_STAMPS
+  Stamps st = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif
   for (uint32_t t = t0; t < t0 + nsteps; t++) {
     if (live && x.l_poison[x.lane] >= t) {
       x.t = t;
       x.b0 = b0;
+#ifdef PXS_STAMPS
+      replica_step<NT, Proto>(P, x, &st);
+#else
       replica_step<NT, Proto>(P, x);
+#endif
     }
     if (++b0 == P.D) b0 = 0;
+#ifdef PXS_STAMPS
+    const unsigned long long sb = stamp();
+#endif
     __syncthreads();
+#ifdef PXS_STAMPS
+    st.barrier += stamp() - sb;
+    st.steps++;
+#endif
   }
+#ifdef PXS_STAMPS
+  if (x.lane == 0 && P.dbg) {
+    unsigned long long* d = &P.dbg[((size_t)blk * 16 + x.r) * 16];
+    atomicAdd(&d[0], st.setup); atomicAdd(&d[1], st.loop); atomicAdd(&d[2], st.barrier);
+    atomicAdd(&d[3], st.trips); atomicAdd(&d[4], st.msgs); atomicAdd(&d[5], st.steps);
+    atomicAdd(&d[6], st.pick); atomicAdd(&d[7], st.disp);
+    atomicAdd(&d[8], st.wait); atomicAdd(&d[9], st.flush);
+  }
+#endif
 
   {
     uint4* g = reinterpret_cast<uint4*>(P.image + (size_t)blk * P.img.bytes);

@@ -1,0 +1,27 @@
+#!/bin/bash
+# rocprofv3 PMC passes for arbitrary counter groups: tools/pmc2.sh <tag> "<grp1>" "<grp2>" ... -- <bench args>
+set -o pipefail
+TAG=$1; shift
+GROUPS_=()
+while [ $# -gt 0 ] && [ "$1" != "--" ]; do GROUPS_+=("$1"); shift; done
+[ "$1" == "--" ] && shift
+R=$(cd "$(dirname "$0")/.." && pwd)
+OUT=$R/gpurun_out/pmc_$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+cd /tmp
+i=0
+for grp in "${GROUPS_[@]}"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --stats -d "$OUT/p$i" -o run --output-format csv -- python "$R/bench.py" --no-cpu-baseline "$@" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
+  python3 - "$OUT/p$i/run_counter_collection.csv" <<'PY'
+import csv, sys, collections
+rows=list(csv.DictReader(open(sys.argv[1])))
+agg=collections.defaultdict(lambda: collections.defaultdict(float))
+for r in rows:
+    if 'sim_steps' not in r['Kernel_Name']: continue
+    agg[int(r['Dispatch_Id'])][r['Counter_Name']]+=float(r['Counter_Value'])
+d=sorted(agg)[-1]
+print(' '.join(f"{k}={v:.4g}" for k,v in agg[d].items()))
+PY
+done
