@@ -1,17 +1,18 @@
 """Headline benchmark (BASELINE.json): simulated messages delivered/s and
-committed slots/s for 1M Multi-Paxos clusters of 5 replicas with Drop/Slow
-fault injection (BASELINE config 2), on 1..8 GPUs.
+committed slots/s, 1M Multi-Paxos clusters of 5 replicas with Drop/Slow fault
+injection per GPU (BASELINE config 2), on 1..8 GPUs.
 
 One bench "step" = one pass of the hot path over the whole batch = one kernel
 launch advancing every cluster of every rank by --sim-steps virtual steps.
 Inputs (cluster state, mailboxes) are resident in HBM before the timed region.
 
-  python bench.py [--gpus N --steps K --warmup W]
+  python bench.py [--gpus N --steps K --warmup W] [--config 2|3|4]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
 
-Multi-GPU: clusters are independent, so each rank owns a contiguous global
-cluster range (PRNG keyed by the global id) and there is no data-path
-collective; RCCL only all-reduces the statistics and the max time.
+--config 3 (ABD + linearizability scan) and --config 4 (FGrid 3x3, leader crash,
+ephemeral leaders) print their own lines; the default is the headline config 2.
+Multi-GPU: see paxi_amd/dist.py — clusters shard by range, no data-path
+collective; RCCL all-reduces the statistics and the max time.
 """
 import argparse
 import json
@@ -24,12 +25,16 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
-# Algorithmic bytes per delivered message: message record
-# written by the sender + read by the receiver, plus the handler's state
-# read-modify-write.  Phase-1 / request / reply records are priced as a
-# record write + read (64 B); P1b payload entries are not counted.
-ALG_BYTES = {"P2a": 160, "P2b": 144, "P3": 192, "P1a": 64, "P1b": 64, "Request": 64, "Reply": 64}
-ALG_BYTES_PER_COMMIT = 64   # leader-side P2a() entry creation
+# Algorithmic bytes per delivered message: the record written by
+# the sender + read by the receiver, plus the handler's state read-modify-write.
+# Multi-Paxos: P2a 160, P2b 144, P3 192 (+64 per committed slot for the leader's
+# P2a() entry); phase-1 / request / reply records priced as a write + read (64).
+# ABD: Get 80, GetReply 144, Set 96, SetReply 128 (+64 per op for the coordinator).
+ALG_BYTES = {"P2a": 160, "P2b": 144, "P3": 192, "P1a": 64, "P1b": 64, "Request": 64, "Reply": 64,
+             "Get": 80, "GetReply": 144, "Set": 96, "SetReply": 128}
+ALG_BYTES_PER_COMMIT = 64
+
+METRIC = "sim messages delivered/sec + committed slots/sec, 1M Paxos clusters, 1-8 GPU"
 
 
 def alg_bytes(delta):
@@ -43,29 +48,47 @@ def stats_delta(a, b):
     return d
 
 
-def config2(args, rank, world, device):
+def workload(cfg_id, clusters, base, device, args):
+    """(cfg, workload, fault process, scripted faults, description) of a BASELINE config."""
     from paxi_amd import abi
-    per = args.clusters
-    cfg = abi.make_config(npz=[5], clusters=per, cluster_base=rank * per, seed=42, window=args.window,
-                          mbox_cap=args.mbox, max_delay=4, steps_per_launch=args.sim_steps, device=device)
-    wl = abi.make_workload(outstanding=8, target=0)
-    fp = abi.make_fault_process(drop_ppm=1000, drop_len=50, slow_ppm=1000, slow_len=50, slow_min=1, slow_max=4)
-    return cfg, wl, fp
+    if cfg_id == 2:
+        cfg = abi.make_config(npz=[5], clusters=clusters, cluster_base=base, seed=42, window=args.window,
+                              mbox_cap=args.mbox, max_delay=4, steps_per_launch=args.sim_steps, device=device)
+        wl = abi.make_workload(outstanding=8, target=0)
+        fp = abi.make_fault_process(drop_ppm=1000, drop_len=50, slow_ppm=1000, slow_len=50, slow_min=1, slow_max=4)
+        return cfg, wl, fp, [], {
+            "workload": "BASELINE config 2: Multi-Paxos 5 replicas x 1M clusters/GPU, Drop/Slow faults",
+            "replicas": 5, "outstanding": 8, "drop": "p=1e-3/step/link, 50-step windows",
+            "slow": "p=1e-3/step/link, 1-4 steps, 50-step windows"}
+    if cfg_id == 3:
+        cfg = abi.make_config(protocol=abi.ABD, npz=[5], clusters=clusters, cluster_base=base, seed=42, keys=16,
+                              mbox_cap=args.mbox, max_delay=4, steps_per_launch=args.sim_steps, device=device,
+                              history=args.history)
+        wl = abi.make_workload(outstanding=4, target=[0, 1, 2, 3], write_ppm=500_000)
+        return cfg, wl, None, [], {
+            "workload": "BASELINE config 3: ABD 5 replicas x 1M clusters/GPU, 16 keys, 50% writes, "
+                        "linearizability scan on device", "replicas": 5, "outstanding": 4}
+    if cfg_id == 4:
+        cfg = abi.make_config(npz=[3, 3, 3], clusters=clusters, cluster_base=base, seed=42, q1=abi.Q_FGRID_Q1,
+                              q2=abi.Q_FGRID_Q2, fz=1, ephemeral_leader=1, window=args.window, mbox_cap=24,
+                              max_delay=0, steps_per_launch=args.sim_steps, device=device)
+        wl = abi.make_workload(outstanding=4, target=[0, 0, 3, 3])
+        faults = [abi.make_fault(abi.FAULT_CRASH, 0, step_from=args.crash_step)]
+        return cfg, wl, None, faults, {
+            "workload": "BASELINE config 4: FGrid 3x3 (fz=1) x 512K clusters/GPU, ephemeral leaders, "
+                        f"leader 1.1 crashed at step {args.crash_step}", "replicas": 9, "outstanding": 4}
+    raise SystemExit(f"unknown config {cfg_id}")
 
 
 def cpu_baseline(args):
-    """The C oracle (same delivery schedule) on a bounded sample of config 2."""
+    """The C oracle (same delivery schedule) on a bounded sample of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
-    from paxi_amd import abi
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    clusters = args.cpu_clusters
-    cfg = abi.make_config(npz=[5], clusters=clusters, seed=42, window=args.window, mbox_cap=args.mbox, max_delay=4)
-    wl = abi.make_workload(outstanding=8, target=0)
-    fp = abi.make_fault_process(drop_ppm=1000, drop_len=50, slow_ppm=1000, slow_len=50, slow_min=1, slow_max=4)
+    cfg, wl, fp, faults, _ = workload(args.config, args.cpu_clusters, 0, 0, args)
     out = {}
     for nthr in (1, threads):
-        o = oracle_lib.OracleSim(cfg, wl, fp)
+        o = oracle_lib.OracleSim(cfg, wl, fp, faults)
         o.step(args.warmup * args.sim_steps, threads=nthr)     # same warm-up as the GPU leg
         s0 = o.stats().as_dict()
         t0 = time.perf_counter()
@@ -84,12 +107,11 @@ def cpu_baseline(args):
                 break
     except OSError:
         pass
-    return {"value": v, "unit": "messages/s", "cores": threads, "kind": "port",
-            "commits_per_s": c,
+    return {"value": v, "unit": "messages/s", "cores": threads, "kind": "port", "commits_per_s": c,
             "single_thread_value": v1,
-            "sample": (f"C oracle (oracle/oracle.c), config 2 on {clusters} clusters x {args.cpu_steps} steps after "
-                       f"{args.warmup * args.sim_steps} warm-up steps; {threads} threads {dt:.1f}s, 1 thread "
-                       f"{dt1:.1f}s ({v1:.3g} msg/s); CPU {cpu}; GOMAXPROCS n/a (no Go toolchain)")}
+            "sample": (f"C oracle (oracle/oracle.c), config {args.config} on {args.cpu_clusters} clusters x "
+                       f"{args.cpu_steps} steps after {args.warmup * args.sim_steps} warm-up steps; {threads} threads "
+                       f"{dt:.1f}s, 1 thread {dt1:.1f}s ({v1:.3g} msg/s); CPU {cpu}; GOMAXPROCS n/a (no Go toolchain)")}
 
 
 def main():
@@ -97,22 +119,27 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=4)
-    ap.add_argument("--clusters", type=int, default=1 << 20, help="clusters per GPU")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4])
+    ap.add_argument("--clusters", type=int, default=None, help="clusters per GPU (default: the config's)")
     ap.add_argument("--sim-steps", type=int, default=50, help="virtual steps per bench step (per launch)")
     ap.add_argument("--window", type=int, default=16)
     ap.add_argument("--mbox", type=int, default=16)
+    ap.add_argument("--history", type=int, default=512, help="config 3: ops recorded per replica")
+    ap.add_argument("--crash-step", type=int, default=1000, help="config 4: step of the leader crash")
     ap.add_argument("--cpu-clusters", type=int, default=16384)
     ap.add_argument("--cpu-steps", type=int, default=1600)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    if args.clusters is None:
+        args.clusters = {2: 1 << 20, 3: 1 << 20, 4: 1 << 19}[args.config]
 
     import torch
     import torch.distributed as dist
+    from paxi_amd import abi
+    from paxi_amd import dist as pdist
     from paxi_amd.sim import Simulation
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = pdist.env_rank()
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
@@ -123,8 +150,9 @@ def main():
         if world > 1:
             dist.barrier()
 
-    cfg, wl, fp = config2(args, rank, world, local)
-    sim = Simulation(cfg, wl, fp)
+    base, count = pdist.shard(args.clusters, rank)
+    cfg, wl, fp, faults, desc = workload(args.config, count, base, local, args)
+    sim = Simulation(cfg, wl, fp, faults)
     for _ in range(args.warmup):
         sim.step(args.sim_steps)
     sim.sync()
@@ -144,23 +172,24 @@ def main():
     s1 = sim.stats().as_dict()
     d = stats_delta(s0, s1)
     violations = sim.check()
+    lin = None
+    if args.config == 3:
+        tl = time.perf_counter()
+        a, n, skipped = sim.linearizable()
+        lin = {"anomalies": a, "ops_checked": n, "partitions_skipped": skipped, "scan_s": time.perf_counter() - tl}
 
-    # whole-job aggregates over RCCL: sum of work, max of time
-    vec = torch.tensor([d["delivered_total"], d["commits"], alg_bytes(d), violations,
-                        s1["flagged"][4], s1["flagged"][5]], dtype=torch.float64, device="cuda")
-    tmax = torch.tensor([dt, kms], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(vec, op=dist.ReduceOp.SUM)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    msgs, commits, abytes, viol, unfaithful, poison = vec.tolist()
-    dt_max, kms_max = tmax.tolist()
+    tot, (dt_max, kms_max) = pdist.reduce_counters(
+        pdist.stats_counters(d, alg_bytes(d), violations, s1["flagged"]), [dt, kms], device="cuda")
 
     if rank == 0:
         avg_launch_ms = kms / max(1, launches)
-        achieved = alg_bytes(d) / max(1, launches) / (avg_launch_ms / 1e3) / 1e9   # rank-0 kernel, GB/s
+        achieved = alg_bytes(d) / max(1, launches) / (avg_launch_ms / 1e3) / 1e9   # rank 0's kernel, GB/s
+        proto = "AbdProto" if args.config == 3 else "PaxosProto"
+        desc.update({"clusters_per_gpu": args.clusters, "sim_steps_per_step": args.sim_steps,
+                     "window": args.window, "mbox_cap": cfg.mbox_cap, "parallelism": f"cluster-sharded x{world}"})
         out = {
-            "metric": "sim messages delivered/sec + committed slots/sec, 1M Paxos clusters, 1-8 GPU",
-            "value": msgs / dt_max,
+            "metric": METRIC,
+            "value": tot["delivered_total"] / dt_max,
             "unit": "messages/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -171,22 +200,20 @@ def main():
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (seeded closed-loop workload, PRNG-keyed faults)",
-            "config": {"workload": "BASELINE config 2: Multi-Paxos 5 replicas x 1M clusters/GPU, Drop/Slow faults",
-                       "clusters_per_gpu": args.clusters, "replicas": 5, "outstanding": 8,
-                       "sim_steps_per_step": args.sim_steps, "window": args.window, "mbox_cap": args.mbox,
-                       "drop": "p=1e-3/step/link, 50-step windows", "slow": "p=1e-3/step/link, 1-4 steps, 50-step windows",
-                       "parallelism": f"cluster-sharded x{world}"},
-            "commits_per_s": commits / dt_max,
+            "config": desc,
+            "commits_per_s": tot["commits"] / dt_max,
             "sim_steps_per_s": args.sim_steps * args.steps / dt_max,
-            "agreement_violations": int(viol),
-            "unfaithful_clusters": int(unfaithful),
-            "poisoned_clusters": int(poison),
+            "agreement_violations": int(tot["violations"]),
+            "unfaithful_clusters": int(tot["unfaithful"]),
+            "poisoned_clusters": int(tot["poisoned"]),
             "kernel_ms_per_step": kms_max / args.steps,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "paxos_steps<5>", "avg_launch_ms": avg_launch_ms,
-                         "alg_bytes_per_launch": alg_bytes(d) / max(1, launches)},
+                         "kernel": f"sim_steps<{abi.n_replicas(cfg)},{proto}>",
+                         "avg_launch_ms": avg_launch_ms, "alg_bytes_per_launch": alg_bytes(d) / max(1, launches)},
         }
+        if lin is not None:
+            out["linearizability"] = lin
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)

@@ -144,9 +144,40 @@ template <int NT>
 __device__ __forceinline__ void intent_flush(const Params& P, Rep<NT>& x) {
   if (!x.im) return;
   constexpr uint32_t NU = NT ? (uint32_t)NT : (uint32_t)PAXISIM_MAX_N;
+  // pass 1: the bucket count of every destination (independent LDS reads:
+  // each destination has its own box, so reading them up front is exact)
+  uint32_t box[NU], k[NU];
 #pragma unroll
-  for (uint32_t d = 0; d < NU; d++)
-    if (d < nrep<NT>(P) && ((x.im >> d) & 1u)) send1<NT>(P, x, d, x.iw0, x.iw1, x.iw2, x.iw3);
+  for (uint32_t d = 0; d < NU; d++) {
+    box[d] = 0;
+    k[d] = 0;
+    if (d < nrep<NT>(P) && ((x.im >> d) & 1u)) {
+      uint32_t b = x.b0 + 1u + (uint32_t)((x.dly >> (4u * d)) & 15u);
+      if (b >= P.D) b -= P.D;
+      box[d] = (b * nrep<NT>(P) + d) * P.NS + x.r;
+      k[d] = x.l_cnt[(box[d] << 6) | x.lane];
+    }
+  }
+  // pass 2: the socket filter and the append, destinations in index order
+#pragma unroll
+  for (uint32_t d = 0; d < NU; d++) {
+    if (!(d < nrep<NT>(P) && ((x.im >> d) & 1u))) continue;
+    const uint32_t seq = x.send_seq++;
+    x.sent++;
+    if ((x.dmask >> d) & 1u) { x.dropped++; continue; }
+    if ((x.fmask >> d) & 1u) {
+      uint32_t p = 0;
+      scripted(P, PAXISIM_FAULT_FLAKY, x.gid, x.r, d, x.t, &p);
+      if (ppm_hit(draw(x.hs, tag(PUR_FLAKY, x.r, seq)), p)) { x.dropped++; continue; }
+    }
+    if (k[d] + 1u > P.M) {
+      x.flags |= PAXISIM_F_MBOX_OVF | PAXISIM_F_UNFAITHFUL;
+      x.dropped++;
+      continue;
+    }
+    x.l_cnt[(box[d] << 6) | x.lane] = (uint8_t)(k[d] + 1u);
+    x.rec[((box[d] * P.M + k[d]) << 6) | x.lane] = make_uint4(x.iw0, x.iw1, x.iw2, x.iw3);
+  }
   x.im = 0;
 }
 template <int NT>

@@ -1,0 +1,46 @@
+"""Multi-GPU orchestration: one process per GPU, clusters sharded by range.
+
+Clusters never exchange messages, so the data path has no collective.  Each
+rank simulates the global cluster range [rank*C, (rank+1)*C) — the PRNG is keyed
+by the global cluster id, so a cluster's trajectory does not
+depend on the number of ranks — and torch.distributed all-reduces only the
+statistics (sum) and the elapsed time (max).  With backend "nccl" that is RCCL
+over xGMI on MI355X; tests use "gloo" on the CPU.
+"""
+import os
+
+# order of the per-rank counter vector that gets all-reduced
+COUNTERS = ("delivered_total", "commits", "replies", "dropped", "client_requests", "alg_bytes",
+            "violations", "unfaithful", "poisoned")
+
+
+def env_rank():
+    """(rank, world, local_rank) from the torchrun environment (defaults: single process)."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def shard(clusters_per_rank, rank):
+    """Global cluster range of one rank under weak scaling: (cluster_base, count)."""
+    return rank * clusters_per_rank, clusters_per_rank
+
+
+def reduce_counters(values, elapsed, device=None, group=None):
+    """Sum `values` (dict over COUNTERS) and max `elapsed` (list of floats) over
+    all ranks.  Returns (summed dict, maxed list).  No-op without a process group."""
+    import torch
+    import torch.distributed as dist
+    vec = torch.tensor([float(values.get(k, 0)) for k in COUNTERS], dtype=torch.float64, device=device)
+    tim = torch.tensor([float(e) for e in elapsed], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(vec, op=dist.ReduceOp.SUM, group=group)
+        dist.all_reduce(tim, op=dist.ReduceOp.MAX, group=group)
+    return dict(zip(COUNTERS, vec.tolist())), tim.tolist()
+
+
+def stats_counters(delta, alg_bytes=0, violations=0, flagged=None):
+    """Counter dict from a stats delta (bench.stats_delta) and scan results."""
+    flagged = flagged or [0] * 8
+    return {"delivered_total": delta["delivered_total"], "commits": delta["commits"], "replies": delta["replies"],
+            "dropped": delta["dropped"], "client_requests": delta["client_requests"], "alg_bytes": alg_bytes,
+            "violations": violations, "unfaithful": flagged[4], "poisoned": flagged[5]}
