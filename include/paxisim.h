@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PAXISIM_ABI_VERSION 2
+#define PAXISIM_ABI_VERSION 3
 
 #define PAXISIM_MAX_N        16  /* replicas per cluster (ack masks are u16) */
 #define PAXISIM_MAX_ZONES    16
@@ -116,17 +116,18 @@ typedef struct paxisim_config {
   uint32_t n_zones;           /* Z (config.go:113) */
   uint32_t npz[PAXISIM_MAX_ZONES]; /* nodes per zone; replica ids are "z.n", z,n >= 1,
                                       indexed in IDs.Less order (id.go:61-69) */
-  uint32_t q1, q2;            /* enum paxisim_quorum for phase 1 / phase 2 */
+  uint32_t q1, q2;            /* enum paxisim_quorum for phase 1 / phase 2; WPaxos derives
+                                 them from fz: GridRow/GridColumn or FGridQ1/Q2 (kpaxos.go:15-27) */
   uint32_t fz;                /* FGrid f_z (wpaxos/replica.go:11) */
   uint32_t thrifty;           /* config.Thrifty (paxos.go:126) */
   uint32_t ephemeral_leader;  /* -ephemeral_leader (paxos/replica.go:12) */
   uint32_t reply_when_commit; /* Paxos.ReplyWhenCommit (paxos.go:37) */
   uint32_t adaptive;          /* WPaxos -adaptive (wpaxos/replica.go:10) */
-  uint32_t policy_threshold;  /* consecutive policy n (policy.go:55-69) */
+  uint32_t policy_threshold;  /* WPaxos consecutive policy n (policy.go:55-69); 0 = null policy */
   uint32_t window;            /* W: log window per replica (power of 2, 8..64) */
   uint32_t mbox_cap;          /* M: records per (link, arrival-step) bucket */
   uint32_t max_delay;         /* largest Slow delay in steps (<= PAXISIM_MAX_DELAY) */
-  uint32_t keys;              /* keys per cluster (ABD/WPaxos instances) */
+  uint32_t keys;              /* keys per cluster (ABD <= 64; WPaxos kpaxos instances <= 32) */
   uint32_t steps_per_launch;  /* HIP backend: steps fused per kernel launch (0 = auto) */
   uint32_t history;           /* ABD: completed ops recorded per replica (0 = none) */
   int32_t  device;            /* HIP device ordinal */
@@ -160,7 +161,10 @@ typedef struct paxisim_fault {
   uint32_t step_from, step_to;     /* active for step_from <= t < step_to */
 } paxisim_fault;
 
-/* Per-replica snapshot (read_state). */
+/* Per-replica snapshot (read_state).  WPaxos replicas aggregate their key
+ * instances: ballot = highest, slot = keys led (Replica.keys, replica.go:110-118),
+ * execute = total executed, active = active instances, p1_acks = mask of
+ * existing instances, npending = total pending, digest = chain of key digests. */
 typedef struct paxisim_replica_state {
   uint64_t ballot;            /* 64-bit Ballot (ballot.go:15-17) */
   int32_t  slot;              /* highest slot (paxos.go:30) */
@@ -180,6 +184,19 @@ typedef struct paxisim_replica_state {
   uint32_t executed_writes;   /* reserved */
   uint32_t pad;
 } paxisim_replica_state;
+
+/* One Paxos instance (read_instances): the single paxos.Paxos of a Multi-Paxos
+ * replica, or one kpaxos per key of a WPaxos replica (wpaxos/kpaxos.go:9-14). */
+typedef struct paxisim_instance_state {
+  uint64_t ballot;            /* 64-bit Ballot */
+  int32_t  slot, execute;
+  uint32_t active;
+  uint32_t exists;            /* WPaxos: r.paxi[key] != nil (Replica.init, replica.go:36-40) */
+  uint32_t p1_acks, npending;
+  uint64_t digest;            /* hash chain of executed (slot, command) */
+  uint32_t policy_last;       /* consecutive policy (policy.go:49-69): last id, 0xFF = "" */
+  uint32_t policy_hits;
+} paxisim_instance_state;
 
 /* Whole-handle totals (sum over clusters and replicas). */
 typedef struct paxisim_stats {
@@ -220,8 +237,15 @@ int  paxisim_stats_get(paxisim* h, paxisim_stats* out);
 int  paxisim_read_state(paxisim* h, uint64_t cluster_lo, uint64_t n,
                         paxisim_replica_state* out);
 
+/* Per-instance snapshot of local clusters [cluster_lo, cluster_lo+n): out has
+ * n*N*I records (I = keys for WPaxos, else 1), cluster-major, then replica,
+ * then key. */
+int  paxisim_read_instances(paxisim* h, uint64_t cluster_lo, uint64_t n,
+                            paxisim_instance_state* out);
+
 /* Agreement scan (client.go:279-320 / tla Safety): number of clusters in
- * which two replicas executed different commands in the same slot. */
+ * which two replicas executed different commands in the same slot (of the
+ * same key, for WPaxos). */
 int  paxisim_check(paxisim* h, uint64_t* violations);
 
 /* Device time of the step kernels since the last reset (HIP events on the

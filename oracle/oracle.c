@@ -122,7 +122,8 @@ int oracle_quorum(uint32_t kind, uint32_t fz, uint32_t n_zones, const uint32_t* 
 typedef struct { uint32_t hdr, ballot, slot, cid; } rec_t;   /* 16-B message record */
 #define HDR(type, n) ((uint32_t)(type) | ((uint32_t)(n) << 8))
 #define HDR_TYPE(h) ((h) & 0xFFu)
-#define HDR_N(h) ((h) >> 8)
+#define HDR_N(h) (((h) >> 8) & 0xFFu)
+#define HDR_KEY(h) ((h) >> 16)       /* WPaxos key (wpaxos/msg.go Key fields) */
 
 /* log entry (paxos/paxos.go:11-18): ballot, command, request, quorum, commit */
 typedef struct { uint32_t ballot, cmd, req, meta; } entry_t;
@@ -140,6 +141,7 @@ typedef struct { uint32_t ballot, cmd, req, meta; } entry_t;
 #define PMAX 32
 #define FMAX 32
 #define KMAX 64  /* ABD keys per cluster */
+#define WP_KMAX 32  /* WPaxos keys (kpaxos instances) per cluster */
 #define CKI 16   /* checkpoint every CKI executed slots */
 #define CKR 8    /* checkpoints kept per replica */
 
@@ -149,30 +151,41 @@ enum { ABD_FREE = 0, ABD_GET = 1, ABD_SET = 2, ABD_DONE = 3 };
 /* one completed client operation (operation.go:5-11), for History.Linearizable */
 typedef struct { uint32_t key, is_write, value, start, end; } hist_t;
 
-typedef struct replica {
-  /* paxos.Paxos fields (paxos/paxos.go:21-38) */
+/* One paxos.Paxos instance (paxos/paxos.go:21-38).  Paxos: one per replica;
+ * WPaxos: one kpaxos per (replica, key) (wpaxos/kpaxos.go:9-14), created on
+ * first use by Replica.init (wpaxos/replica.go:37-41). */
+typedef struct inst {
   uint32_t ballot;
   int32_t slot, execute;
   uint32_t active;
   uint32_t p1mask;                 /* p.quorum (phase 1) */
   uint32_t npend, pend[PMAX];      /* p.requests */
   entry_t* log;                    /* p.log, window [execute, execute+W) */
-  /* node.forwards (node.go:35, 165-172) */
-  uint32_t nfwd, fwd[FMAX];
-  /* socket fault state (socket.go:26-34), random process */
-  uint32_t drop_until[PAXISIM_MAX_N], slow_until[PAXISIM_MAX_N], slow_delay[PAXISIM_MAX_N];
   /* executed-history digest + checkpoints */
   uint64_t digest;
   uint32_t ck_e[CKR];
   uint64_t ck_d[CKR];
+  /* exec log (KATs) */
+  uint32_t* xlog;
+  uint32_t nx, capx;
+  /* WPaxos: r.paxi[key] != nil, and the consecutive policy (policy.go:49-69) */
+  uint32_t exists, pol_last, pol_hits;
+  uint32_t iflags;                 /* WOVF / GHOST raised on this instance's log */
+  /* Uncommitted ghost entries Go would hold below execute: slot range and ballot range */
+  uint32_t glo, ghi, gmin, gmax;
+} inst_t;
+
+typedef struct replica {
+  inst_t* inst;                    /* NK instances (key-major) */
+  /* node.forwards (node.go:35, 165-172) */
+  uint32_t nfwd, fwd[FMAX];
+  /* socket fault state (socket.go:26-34), random process */
+  uint32_t drop_until[PAXISIM_MAX_N], slow_until[PAXISIM_MAX_N], slow_delay[PAXISIM_MAX_N];
   uint32_t flags;
   uint32_t send_seq;
   /* counters */
   uint32_t delivered[PAXISIM_NMSG];
   uint32_t client_requests, sent, dropped, discarded, commits, replies;
-  /* exec log (KATs) */
-  uint32_t* xlog;
-  uint32_t nx, capx;
   /* ABD (abd/replica.go:28-34): cid counter, versioned KV, op table */
   uint32_t abd_cid;
   uint32_t *kv_val, *kv_ver;
@@ -204,13 +217,17 @@ struct oracle_sim {
   uint32_t t;                      /* next step to simulate */
   int keep_xlog;
   uint32_t OW;                     /* ABD op table size */
+  uint32_t NK;                     /* Paxos instances per replica: WPaxos keys, else 1 */
+  uint32_t q1, q2;                 /* quorum kinds in use (WPaxos: from fz, wpaxos/kpaxos.go:16-28) */
 };
 
 /* handler context: one replica of one cluster at one step */
 typedef struct ctx {
   const struct oracle_sim* s;
   cluster_t* c;
-  replica_t* p;
+  replica_t* n;                    /* the node (paxi.Node: socket, forwards, counters) */
+  inst_t* p;                       /* the bound Paxos instance */
+  uint32_t ktag;                   /* WPaxos: key << 16, tagged onto P1a..P3 records */
   uint32_t r, t, hs;
   int stop;                        /* replica panicked in this step */
 } ctx_t;
@@ -224,7 +241,10 @@ static inline uint8_t* mb_cnt(const struct oracle_sim* s, cluster_t* c, uint32_t
   return &c->cnt[((size_t)b * s->N + dst) * s->NS + src];
 }
 
-static inline void raise_flag(ctx_t* x, uint32_t f) { x->p->flags |= f; }
+static inline void raise_flag(ctx_t* x, uint32_t f) {
+  x->n->flags |= f;
+  x->p->iflags |= f & (PAXISIM_F_WOVF | PAXISIM_F_GHOST);   /* window flags are per instance */
+}
 
 /* ------------------------------------------------------------------------ */
 /* Fault filter (socket.go:66-109): crash -> drop -> flaky -> slow           */
@@ -251,7 +271,7 @@ static int crashed(const struct oracle_sim* s, const cluster_t* c, uint32_t r, u
 /* socket.Send (socket.go:66-109) with the bucketed mailbox of DESIGN.md §3.2. */
 static void sock_send(ctx_t* x, uint32_t to, const rec_t* recs, uint32_t nrec) {
   const struct oracle_sim* s = x->s;
-  replica_t* p = x->p;
+  replica_t* p = x->n;
   uint32_t seq = p->send_seq++, delay = 0, flaky = 0, b;
   uint8_t* cnt;
   p->sent++;
@@ -315,7 +335,7 @@ static void client_reply(ctx_t* x, uint32_t cid) {
   const struct oracle_sim* s = x->s;
   uint32_t WK = s->wl.outstanding, w = (cid - 1u) % WK;
   if (x->c->wk_cur[w] != cid) return;                /* duplicate reply: worker moved on */
-  x->p->replies++;
+  x->n->replies++;
   if (s->wl.max_requests == 0 || x->c->wk_issued[w] < s->wl.max_requests) {
     uint64_t nc = 1ull + w + (uint64_t)WK * x->c->wk_issued[w];
     if (nc > CID_MAX) { raise_flag(x, PAXISIM_F_PEND_OVF | PAXISIM_F_UNFAITHFUL); x->c->wk_cur[w] = 0; return; }
@@ -337,7 +357,7 @@ static void request_reply(ctx_t* x, uint32_t req, uint32_t reply_cmd) {
 
 /* node.Forward (node.go:165-172): remember the request, send it to id. */
 static void node_forward(ctx_t* x, uint32_t to, uint32_t req) {
-  replica_t* p = x->p;
+  replica_t* p = x->n;
   uint32_t i, cid = REQ_CID(req);
   for (i = 0; i < p->nfwd; i++)
     if (REQ_CID(p->fwd[i]) == cid) break;
@@ -352,7 +372,7 @@ static void node_forward(ctx_t* x, uint32_t to, uint32_t req) {
 
 /* node.recv Reply case (node.go:83-90): forwards[cmd].Reply(m). */
 static void handle_reply(ctx_t* x, uint32_t cid) {
-  replica_t* p = x->p;
+  replica_t* p = x->n;
   uint32_t i;
   for (i = 0; i < p->nfwd; i++)
     if (REQ_CID(p->fwd[i]) == cid) break;
@@ -376,35 +396,54 @@ static inline int in_window(const ctx_t* x, int32_t s) {
 static inline entry_t* log_at(const ctx_t* x, int32_t s) { return &x->p->log[(uint32_t)s & (x->s->W - 1u)]; }
 static inline int q1_ok(const ctx_t* x, uint32_t m) {
   const struct oracle_sim* s = x->s;
-  return quorum_eval(s->cfg.q1, s->cfg.fz, s->Z, s->cfg.npz, s->zmask, s->N, m);
+  return quorum_eval(s->q1, s->cfg.fz, s->Z, s->cfg.npz, s->zmask, s->N, m);
 }
 static inline int q2_ok(const ctx_t* x, uint32_t m) {
   const struct oracle_sim* s = x->s;
-  return quorum_eval(s->cfg.q2, s->cfg.fz, s->Z, s->cfg.npz, s->zmask, s->N, m);
+  return quorum_eval(s->q2, s->cfg.fz, s->Z, s->cfg.npz, s->zmask, s->N, m);
 }
 static inline int is_leader(const ctx_t* x) {             /* Paxos.IsLeader paxos.go:61-63 */
   return x->p->active || bal_id(x->p->ballot) == x->r;
 }
 
+/* An entry Go would create or update below execute (a "ghost": update() or
+ * HandleP2a on a slot already executed here) is not stored.  A ghost is inert
+ * except to HandleP2b (paxos.go:270-310), which for m.Ballot >= e.ballot
+ * adopts a higher ballot or, on m.Ballot == e.ballot owned by self, panics on
+ * the nil quorum; the summary below makes that observation detectable. */
+static void ghost(ctx_t* x, int32_t s, uint32_t b) {
+  inst_t* p = x->p;
+  raise_flag(x, PAXISIM_F_GHOST);
+  if ((uint32_t)s < p->glo) p->glo = (uint32_t)s;
+  if ((uint32_t)s > p->ghi) p->ghi = (uint32_t)s;
+  if (b < p->gmin) p->gmin = b;
+  if (b > p->gmax) p->gmax = b;
+}
+static int ghost_observed(const ctx_t* x, int32_t ms, uint32_t mb) {
+  const inst_t* p = x->p;
+  if ((uint32_t)ms < p->glo || (uint32_t)ms > p->ghi || mb < p->gmin) return 0;
+  return mb > p->ballot || (bal_id(mb) == x->r && mb <= p->gmax);
+}
+
 static void paxos_forward(ctx_t* x) {                     /* paxos.go:371-376 */
-  replica_t* p = x->p;
+  inst_t* p = x->p;
   uint32_t i;
   for (i = 0; i < p->npend; i++) node_forward(x, bal_id(p->ballot), p->pend[i]);
   p->npend = 0;
 }
 
 static void paxos_p1a(ctx_t* x) {                         /* paxos.go:100-108 */
-  replica_t* p = x->p;
+  inst_t* p = x->p;
   if (p->active) return;
   if ((p->ballot >> 4) + 1u >= (1u << 27)) raise_flag(x, PAXISIM_F_BALLOT_OVF | PAXISIM_F_UNFAITHFUL);
   p->ballot = bal_next(p->ballot, x->r);
   p->p1mask = 1u << x->r;
-  broadcast1(x, PAXISIM_MSG_P1A, p->ballot, 0, 0);
+  broadcast1(x, PAXISIM_MSG_P1A | x->ktag, p->ballot, 0, 0);
 }
 
 static void paxos_p2a(ctx_t* x, uint32_t req) {           /* paxos.go:111-131 */
   const struct oracle_sim* s = x->s;
-  replica_t* p = x->p;
+  inst_t* p = x->p;
   p->slot++;
   if (in_window(x, p->slot)) {
     entry_t* e = log_at(x, p->slot);
@@ -415,12 +454,12 @@ static void paxos_p2a(ctx_t* x, uint32_t req) {           /* paxos.go:111-131 */
   } else {
     raise_flag(x, PAXISIM_F_WOVF | PAXISIM_F_UNFAITHFUL);  /* request lost */
   }
-  if (s->cfg.thrifty) multicast_quorum1(x, s->N / 2 + 1, PAXISIM_MSG_P2A, p->ballot, (uint32_t)p->slot, REQ_CID(req));
-  else broadcast1(x, PAXISIM_MSG_P2A, p->ballot, (uint32_t)p->slot, REQ_CID(req));
+  if (s->cfg.thrifty) multicast_quorum1(x, s->N / 2 + 1, PAXISIM_MSG_P2A | x->ktag, p->ballot, (uint32_t)p->slot, REQ_CID(req));
+  else broadcast1(x, PAXISIM_MSG_P2A | x->ktag, p->ballot, (uint32_t)p->slot, REQ_CID(req));
 }
 
 static void paxos_handle_request(ctx_t* x, uint32_t req) { /* paxos.go:86-97 */
-  replica_t* p = x->p;
+  inst_t* p = x->p;
   if (!p->active) {
     if (p->npend == PMAX) raise_flag(x, PAXISIM_F_PEND_OVF | PAXISIM_F_UNFAITHFUL);
     else p->pend[p->npend++] = req;
@@ -441,7 +480,7 @@ static void replica_handle_request(ctx_t* x, uint32_t req) {
 static void paxos_exec(ctx_t* x);
 
 static void paxos_handle_p1a(ctx_t* x, uint32_t mb) {      /* paxos.go:134-162 */
-  replica_t* p = x->p;
+  inst_t* p = x->p;
   rec_t out[1 + PAXISIM_MAX_WINDOW];
   uint32_t n = 0;
   int32_t s, hi;
@@ -450,7 +489,7 @@ static void paxos_handle_p1a(ctx_t* x, uint32_t mb) {      /* paxos.go:134-162 *
     p->active = 0;
     paxos_forward(x);
   }
-  if (p->flags & PAXISIM_F_WOVF) raise_flag(x, PAXISIM_F_UNFAITHFUL);  /* Go may hold skipped entries */
+  if (x->p->iflags & PAXISIM_F_WOVF) raise_flag(x, PAXISIM_F_UNFAITHFUL);  /* Go may hold skipped entries */
   hi = p->slot;
   if (hi > p->execute + (int32_t)x->s->W - 1) hi = p->execute + (int32_t)x->s->W - 1;
   for (s = p->execute; s <= hi; s++) {
@@ -462,7 +501,7 @@ static void paxos_handle_p1a(ctx_t* x, uint32_t mb) {      /* paxos.go:134-162 *
     out[n].slot = (uint32_t)s;
     out[n].cid = e->cmd;
   }
-  out[0].hdr = HDR(PAXISIM_MSG_P1B, n);
+  out[0].hdr = HDR(PAXISIM_MSG_P1B, n) | x->ktag;
   out[0].ballot = p->ballot;
   out[0].slot = 0;
   out[0].cid = 0;
@@ -470,7 +509,7 @@ static void paxos_handle_p1a(ctx_t* x, uint32_t mb) {      /* paxos.go:134-162 *
 }
 
 static void paxos_update(ctx_t* x, const rec_t* log, uint32_t n) { /* paxos.go:164-180 */
-  replica_t* p = x->p;
+  inst_t* p = x->p;
   uint32_t i;
   for (i = 0; i < n; i++) {
     int32_t s = (int32_t)log[i].slot;
@@ -489,7 +528,7 @@ static void paxos_update(ctx_t* x, const rec_t* log, uint32_t n) { /* paxos.go:1
         e->meta = E_EXISTS;                                /* quorum nil */
       }
     } else if (s < p->execute) {
-      raise_flag(x, PAXISIM_F_GHOST);
+      ghost(x, s, log[i].ballot);
     } else {
       raise_flag(x, PAXISIM_F_WOVF);
     }
@@ -497,7 +536,7 @@ static void paxos_update(ctx_t* x, const rec_t* log, uint32_t n) { /* paxos.go:1
 }
 
 static void paxos_handle_p1b(ctx_t* x, uint32_t src, uint32_t mb, const rec_t* log, uint32_t n) { /* paxos.go:183-230 */
-  replica_t* p = x->p;
+  inst_t* p = x->p;
   if (mb < p->ballot || p->active) return;
   paxos_update(x, log, n);
   if (mb > p->ballot) {
@@ -512,7 +551,7 @@ static void paxos_handle_p1b(ctx_t* x, uint32_t src, uint32_t mb, const rec_t* l
       uint32_t k, npend;
       uint32_t pend[PMAX];
       p->active = 1;
-      if (p->flags & PAXISIM_F_WOVF) raise_flag(x, PAXISIM_F_UNFAITHFUL);
+      if (x->p->iflags & PAXISIM_F_WOVF) raise_flag(x, PAXISIM_F_UNFAITHFUL);
       hi = p->slot;
       if (hi > p->execute + (int32_t)x->s->W - 1) hi = p->execute + (int32_t)x->s->W - 1;
       for (i = p->execute; i <= hi; i++) {
@@ -520,7 +559,7 @@ static void paxos_handle_p1b(ctx_t* x, uint32_t src, uint32_t mb, const rec_t* l
         if (!(e->meta & E_EXISTS) || (e->meta & E_COMMIT)) continue;   /* nil gap skipped (G5) */
         e->ballot = p->ballot;
         e->meta = (e->meta & (E_EXISTS | E_COMMIT)) | E_QUORUM | ((1u << x->r) << 16);
-        broadcast1(x, PAXISIM_MSG_P2A, p->ballot, (uint32_t)i, e->cmd);
+        broadcast1(x, PAXISIM_MSG_P2A | x->ktag, p->ballot, (uint32_t)i, e->cmd);
       }
       npend = p->npend;
       memcpy(pend, p->pend, npend * sizeof(uint32_t));
@@ -531,7 +570,7 @@ static void paxos_handle_p1b(ctx_t* x, uint32_t src, uint32_t mb, const rec_t* l
 }
 
 static void paxos_handle_p2a(ctx_t* x, uint32_t mb, int32_t ms, uint32_t mcid) { /* paxos.go:233-267 */
-  replica_t* p = x->p;
+  inst_t* p = x->p;
   if (mb >= p->ballot) {
     p->ballot = mb;
     p->active = 0;
@@ -554,20 +593,19 @@ static void paxos_handle_p2a(ctx_t* x, uint32_t mb, int32_t ms, uint32_t mcid) {
         e->meta = E_EXISTS;
       }
     } else if (ms < p->execute) {
-      raise_flag(x, PAXISIM_F_GHOST);
+      ghost(x, ms, mb);
     } else {
       raise_flag(x, PAXISIM_F_WOVF);
     }
   }
-  send1(x, bal_id(mb), PAXISIM_MSG_P2B, p->ballot, (uint32_t)ms, 0);
+  send1(x, bal_id(mb), PAXISIM_MSG_P2B | x->ktag, p->ballot, (uint32_t)ms, 0);
 }
 
 static void paxos_handle_p2b(ctx_t* x, uint32_t src, uint32_t mb, int32_t ms) { /* paxos.go:270-310 */
-  replica_t* p = x->p;
+  inst_t* p = x->p;
   entry_t* e;
   if (!in_window(x, ms)) {
-    if ((ms < p->execute && (p->flags & PAXISIM_F_GHOST)) ||
-        (ms >= p->execute && (p->flags & PAXISIM_F_WOVF)))
+    if (ms < p->execute ? ghost_observed(x, ms, mb) : (x->p->iflags & PAXISIM_F_WOVF) != 0)
       raise_flag(x, PAXISIM_F_UNFAITHFUL);
     return;
   }
@@ -586,8 +624,8 @@ static void paxos_handle_p2b(ctx_t* x, uint32_t src, uint32_t mb, int32_t ms) { 
     e->meta |= (1u << src) << 16;
     if (q2_ok(x, E_ACK(e->meta))) {
       e->meta |= E_COMMIT;
-      p->commits++;
-      broadcast1(x, PAXISIM_MSG_P3, mb, (uint32_t)ms, e->cmd);
+      x->n->commits++;
+      broadcast1(x, PAXISIM_MSG_P3 | x->ktag, mb, (uint32_t)ms, e->cmd);
       if (x->s->cfg.reply_when_commit) {
         if (!e->req) { raise_flag(x, PAXISIM_F_POISON); x->stop = 1; return; } /* nil r.Reply */
         request_reply(x, e->req, REQ_CID(e->req));         /* Reply{Command: r.Command} */
@@ -599,7 +637,7 @@ static void paxos_handle_p2b(ctx_t* x, uint32_t src, uint32_t mb, int32_t ms) { 
 }
 
 static void paxos_handle_p3(ctx_t* x, uint32_t mb, int32_t ms, uint32_t mcid) { /* paxos.go:313-343 */
-  replica_t* p = x->p;
+  inst_t* p = x->p;
   if (ms > p->slot) p->slot = ms;
   if (in_window(x, ms)) {
     entry_t* e = log_at(x, ms);
@@ -628,11 +666,11 @@ static void paxos_handle_p3(ctx_t* x, uint32_t mb, int32_t ms, uint32_t mcid) { 
 }
 
 static void paxos_exec(ctx_t* x) {                         /* paxos.go:345-369 */
-  replica_t* p = x->p;
+  inst_t* p = x->p;
   for (;;) {
     entry_t* e = log_at(x, p->execute);
     if (!(e->meta & E_EXISTS) || !(e->meta & E_COMMIT)) break;
-    if (p->flags & PAXISIM_F_WOVF) raise_flag(x, PAXISIM_F_UNFAITHFUL);
+    if (x->p->iflags & PAXISIM_F_WOVF) raise_flag(x, PAXISIM_F_UNFAITHFUL);
     if (e->req) {
       request_reply(x, e->req, e->cmd);
       e->req = 0;
@@ -675,11 +713,109 @@ static void paxos_dispatch(ctx_t* x, uint32_t src, const rec_t* m) {
 /* Workload: key and read/write of command cid (benchmark.go:202-275)        */
 /* ------------------------------------------------------------------------ */
 static inline uint32_t wl_hash(uint32_t kc, uint32_t cid) { return fmix32(fmix32(kc ^ 0x5BD1E995u) ^ cid); }
+/* Key of command cid.  With locality (the WPaxos per-zone clients, each
+ * drawing from its zone's keys: benchmark.go:202-213 "conflict"/Min), worker
+ * w's command is, with P = locality, one of the keys k = z (mod Z) of the zone
+ * z of the replica it sends to, otherwise uniform over all keys. */
 static inline uint32_t wl_key(const struct oracle_sim* s, uint32_t kc, uint32_t cid) {
-  return wl_hash(kc, cid) % s->cfg.keys;
+  const uint32_t h = wl_hash(kc, cid), K = s->cfg.keys;
+  if (s->wl.locality_ppm) {
+    const uint32_t w = (cid - 1u) % s->wl.outstanding;
+    const uint32_t z = s->zone_of[s->wl.target[w]] - 1u, Z = s->Z;
+    const uint32_t nk = z < K ? (K - z + Z - 1u) / Z : 0u;
+    if (nk && ppm_hit(fmix32(h ^ 0x165667B1u), s->wl.locality_ppm)) return z + Z * (h % nk);
+  }
+  return h % K;
 }
 static inline int wl_write(const struct oracle_sim* s, uint32_t kc, uint32_t cid) {
   return ppm_hit(fmix32(wl_hash(kc, cid) ^ 0x27D4EB2Fu), s->wl.write_ppm);
+}
+
+/* ------------------------------------------------------------------------ */
+/* WPaxos (wpaxos/replica.go, wpaxos/kpaxos.go): one Paxos instance per key, */
+/* Q1/Q2 = GridRow/GridColumn (fz = 0) or FGridQ1/Q2(fz) (kpaxos.go:15-27),  */
+/* consecutive leader-migration policy.  The kpaxos Broadcast/Send wrappers  */
+/* (kpaxos.go:51-74) tag P1a..P3 with the key: x->ktag.                      */
+/* ------------------------------------------------------------------------ */
+#define POL_NONE 0xFFu                                     /* ID "" */
+static inline void wp_bind(ctx_t* x, uint32_t key) {
+  x->p = &x->n->inst[key];
+  x->ktag = key << 16;
+}
+static inline void wp_init(ctx_t* x, uint32_t key) {       /* Replica.init replica.go:36-40 */
+  wp_bind(x, key);
+  x->p->exists = 1;
+}
+/* r.paxi[m.Key] without init: a nil *kpaxos, whose use panics in Go */
+static inline int wp_get(ctx_t* x, uint32_t key) {
+  wp_bind(x, key);
+  if (x->p->exists) return 1;
+  raise_flag(x, PAXISIM_F_POISON);
+  x->stop = 1;
+  return 0;
+}
+
+/* consecutive.Hit (policy.go:55-69); threshold 0 is the null policy (policy.go:18-21) */
+static uint32_t policy_hit(ctx_t* x, uint32_t id) {
+  inst_t* p = x->p;
+  uint32_t res = POL_NONE;
+  if (x->s->cfg.policy_threshold == 0) return POL_NONE;
+  if (id == p->pol_last) {
+    p->pol_hits++;
+  } else {
+    p->pol_last = id;
+    p->pol_hits = 1;
+  }
+  if (p->pol_hits >= x->s->cfg.policy_threshold) {
+    res = p->pol_last;
+    p->pol_last = POL_NONE;
+    p->pol_hits = 0;
+  }
+  return res;
+}
+
+static void wp_handle_request(ctx_t* x, uint32_t req) {   /* replica.go:42-66 */
+  const struct oracle_sim* s = x->s;
+  wp_init(x, wl_key(s, x->c->kc, REQ_CID(req)));
+  if (!s->cfg.adaptive) {
+    paxos_handle_request(x, req);
+    return;
+  }
+  if (is_leader(x) || x->p->ballot == 0) {
+    const uint32_t o = REQ_ORIGIN(req);
+    uint32_t to;
+    paxos_handle_request(x, req);
+    /* m.NodeID: the receiving node for an HTTP request (http.go:96), the forwarder otherwise (node.go:167) */
+    to = policy_hit(x, o == PAXISIM_CLIENT_SRC ? x->r : o);
+    if (to != POL_NONE && s->zone_of[to] != s->zone_of[x->r])
+      send1(x, to, PAXISIM_MSG_LEADERCHG | x->ktag, x->p->ballot, to, x->r);   /* LeaderChange{Key,To,From,Ballot} */
+  } else {
+    node_forward(x, bal_id(x->p->ballot), req);            /* `go r.Forward(p.Leader(), m)` */
+  }
+}
+
+static void wp_handle_leader_change(ctx_t* x, uint32_t key, uint32_t mb, uint32_t to) { /* replica.go:101-108 */
+  if (!wp_get(x, key)) return;
+  if (mb == x->p->ballot && to == x->r) paxos_p1a(x);
+}
+
+static void wpaxos_dispatch(ctx_t* x, uint32_t src, const rec_t* m) {   /* registrations replica.go:25-32 */
+  const uint32_t key = HDR_KEY(m->hdr);
+  switch (HDR_TYPE(m->hdr)) {
+    case PAXISIM_MSG_REQUEST:
+      wp_handle_request(x, REQ(m->cid, src == x->s->N ? PAXISIM_CLIENT_SRC : src));
+      break;
+    case PAXISIM_MSG_REPLY: handle_reply(x, m->cid); break;
+    case PAXISIM_MSG_P1A: wp_init(x, key); paxos_handle_p1a(x, m->ballot); break;          /* handlePrepare 72-76 */
+    case PAXISIM_MSG_P1B:                                                                  /* handlePromise 78-82 */
+      if (wp_get(x, key)) paxos_handle_p1b(x, src, m->ballot, m + 1, HDR_N(m->hdr));
+      break;
+    case PAXISIM_MSG_P2A: wp_init(x, key); paxos_handle_p2a(x, m->ballot, (int32_t)m->slot, m->cid); break; /* 84-88 */
+    case PAXISIM_MSG_P2B: if (wp_get(x, key)) paxos_handle_p2b(x, src, m->ballot, (int32_t)m->slot); break; /* 90-93 */
+    case PAXISIM_MSG_P3: wp_init(x, key); paxos_handle_p3(x, m->ballot, (int32_t)m->slot, m->cid); break;   /* 95-99 */
+    case PAXISIM_MSG_LEADERCHG: wp_handle_leader_change(x, key, m->ballot, m->slot); break;
+    default: break;
+  }
 }
 
 /* ------------------------------------------------------------------------ */
@@ -703,7 +839,7 @@ static inline int majority(const ctx_t* x, uint32_t mask) { return popc(mask) > 
 static inline void abd_put(replica_t* p, uint32_t key, uint32_t val) { if (val) p->kv_val[key] = val; }
 
 static void abd_handle_request(ctx_t* x, uint32_t cid) {                    /* abd/replica.go:50-71 */
-  replica_t* p = x->p;
+  replica_t* p = x->n;
   const uint32_t k = wl_key(x->s, x->c->kc, cid);
   abd_op_t* e;
   p->abd_cid++;
@@ -722,11 +858,11 @@ static void abd_handle_request(ctx_t* x, uint32_t cid) {                    /* a
 }
 
 static void abd_handle_get(ctx_t* x, uint32_t src, uint32_t key, uint32_t opid) { /* abd/replica.go:73-82 */
-  abd_send(x, src, PAXISIM_MSG_GETREPLY, key, opid, x->p->kv_ver[key], x->p->kv_val[key]);
+  abd_send(x, src, PAXISIM_MSG_GETREPLY, key, opid, x->n->kv_ver[key], x->n->kv_val[key]);
 }
 
 static void abd_handle_set(ctx_t* x, uint32_t src, uint32_t key, uint32_t opid, uint32_t ver, uint32_t val) { /* 84-95 */
-  replica_t* p = x->p;
+  replica_t* p = x->n;
   if (ver > p->kv_ver[key]) {
     abd_put(p, key, val);
     p->kv_ver[key] = ver;
@@ -735,12 +871,12 @@ static void abd_handle_set(ctx_t* x, uint32_t src, uint32_t key, uint32_t opid, 
 }
 
 static abd_op_t* abd_op(ctx_t* x, uint32_t opid) {
-  abd_op_t* e = &x->p->ops[opid & (x->s->OW - 1u)];
+  abd_op_t* e = &x->n->ops[opid & (x->s->OW - 1u)];
   return e->tag == opid ? e : NULL;   /* a retired op: Go's entry is Done, or was flagged when evicted */
 }
 
 static void abd_handle_getreply(ctx_t* x, uint32_t src, uint32_t key, uint32_t opid, uint32_t ver, uint32_t val) { /* 97-136 */
-  replica_t* p = x->p;
+  replica_t* p = x->n;
   abd_op_t* e = abd_op(x, opid);
   if (!e || e->state != ABD_GET) return;
   if (ver > e->version) {
@@ -772,7 +908,7 @@ static void abd_handle_setreply(ctx_t* x, uint32_t src, uint32_t key, uint32_t o
   e->setmask |= 1u << src;
   if (majority(x, e->setmask)) {
     int w = wl_write(x->s, c->kc, e->req);
-    replica_t* p = x->p;
+    replica_t* p = x->n;
     e->state = ABD_DONE;
     p->commits++;
     if (p->nh < x->s->cfg.history) {                 /* History.AddOperation (history.go:44-52) */
@@ -807,7 +943,7 @@ static void abd_dispatch(ctx_t* x, uint32_t src, const rec_t* m) {
 static void fault_process(ctx_t* x) {
   const struct oracle_sim* s = x->s;
   const paxisim_fault_process* fp = &s->fp;
-  replica_t* p = x->p;
+  replica_t* p = x->n;
   uint32_t d;
   if (fp->drop_ppm == 0 && fp->slow_ppm == 0) return;
   for (d = 0; d < s->N; d++) {
@@ -829,9 +965,10 @@ static void replica_step(const struct oracle_sim* s, cluster_t* c, uint32_t r, u
   ctx_t x;
   uint32_t b = t % s->D, src, rem[PAXISIM_MAX_N + 1], pos[PAXISIM_MAX_N + 1], total = 0, i;
   int crash;
-  x.s = s; x.c = c; x.p = &c->rep[r]; x.r = r; x.t = t; x.stop = 0;
+  x.s = s; x.c = c; x.n = &c->rep[r]; x.p = &x.n->inst[0]; x.ktag = 0;
+  x.r = r; x.t = t; x.stop = 0;
   x.hs = step_key(c->kc, t);
-  x.p->send_seq = 0;
+  x.n->send_seq = 0;
   fault_process(&x);
   crash = crashed(s, c, r, t);
   for (src = 0; src < s->NS; src++) {
@@ -841,7 +978,7 @@ static void replica_step(const struct oracle_sim* s, cluster_t* c, uint32_t r, u
       uint32_t k = 0;
       while (k < rem[src]) {
         rec_t* m = mb_rec(s, c, b, r, src, k);
-        x.p->discarded++;
+        x.n->discarded++;
         k += 1u + (HDR_TYPE(m->hdr) == PAXISIM_MSG_P1B ? HDR_N(m->hdr) : 0u);
       }
       rem[src] = 0;
@@ -858,9 +995,10 @@ static void replica_step(const struct oracle_sim* s, cluster_t* c, uint32_t r, u
     pos[src] += len;
     rem[src] -= len;
     total -= len;
-    if (src == s->N) x.p->client_requests++;
-    else x.p->delivered[HDR_TYPE(m->hdr)]++;
+    if (src == s->N) x.n->client_requests++;
+    else x.n->delivered[HDR_TYPE(m->hdr)]++;
     if (s->cfg.protocol == PAXISIM_ABD) abd_dispatch(&x, src, m);
+    else if (s->cfg.protocol == PAXISIM_WPAXOS) wpaxos_dispatch(&x, src, m);
     else paxos_dispatch(&x, src, m);
   }
   for (src = 0; src < s->NS; src++) *mb_cnt(s, c, b, r, src) = 0;
@@ -879,9 +1017,12 @@ static void cluster_step(const struct oracle_sim* s, cluster_t* c, uint32_t t) {
 static int check_config(const paxisim_config* cfg, const paxisim_workload* wl,
                         const paxisim_fault_process* fp, uint32_t* N_out) {
   uint32_t z, N = 0, w;
-  if (cfg->protocol != PAXISIM_PAXOS && cfg->protocol != PAXISIM_ABD)
-    return fail(PAXISIM_EUNSUPP, "protocol %u not built", cfg->protocol);
+  if (cfg->protocol > PAXISIM_WPAXOS) return fail(PAXISIM_EUNSUPP, "protocol %u not built", cfg->protocol);
   if (cfg->protocol == PAXISIM_ABD && (cfg->keys < 1 || cfg->keys > KMAX)) return fail(PAXISIM_EINVAL, "keys");
+  if (cfg->protocol == PAXISIM_WPAXOS && (cfg->keys < 1 || cfg->keys > WP_KMAX))
+    return fail(PAXISIM_EINVAL, "WPaxos keys must be in [1,%u]", WP_KMAX);
+  if (cfg->policy_threshold > 255) return fail(PAXISIM_EINVAL, "policy_threshold");
+  if (wl->locality_ppm && cfg->keys < 1) return fail(PAXISIM_EINVAL, "locality needs keys");
   if (cfg->n_zones < 1 || cfg->n_zones > PAXISIM_MAX_ZONES) return fail(PAXISIM_EINVAL, "n_zones");
   for (z = 0; z < cfg->n_zones; z++) {
     if (cfg->npz[z] < 1) return fail(PAXISIM_EINVAL, "npz[%u] must be >= 1", z);
@@ -910,15 +1051,23 @@ static uint32_t abd_ow(uint32_t outstanding) {  /* ABD op table: pow2 >= 2*outst
   return ow;
 }
 
-static void cluster_init(struct oracle_sim* s, cluster_t* c, uint64_t gid, entry_t* logs) {
+static void cluster_init(struct oracle_sim* s, cluster_t* c, uint64_t gid, entry_t* logs, inst_t* insts) {
   uint32_t r, w;
   memset(c->rep, 0, sizeof c->rep);
   c->gid = gid;
   c->kc = cluster_key(s->cfg.seed, gid);
   c->poison_step = 0xFFFFFFFFu;
   for (r = 0; r < s->N; r++) {
-    c->rep[r].slot = -1;                                   /* paxos.go:45 */
-    c->rep[r].log = logs + (size_t)r * s->W;
+    uint32_t k;
+    c->rep[r].inst = insts + (size_t)r * s->NK;
+    for (k = 0; k < s->NK; k++) {
+      inst_t* p = &c->rep[r].inst[k];
+      p->slot = -1;                                        /* paxos.go:45 */
+      p->log = logs + ((size_t)r * s->NK + k) * s->W;
+      p->exists = s->cfg.protocol != PAXISIM_WPAXOS;
+      p->pol_last = POL_NONE;
+      p->glo = p->gmin = 0xFFFFFFFFu;
+    }
     if (s->cfg.protocol == PAXISIM_ABD) {
       c->rep[r].kv_val = (uint32_t*)calloc(2u * s->cfg.keys, sizeof(uint32_t));
       c->rep[r].kv_ver = c->rep[r].kv_val + s->cfg.keys;
@@ -964,15 +1113,35 @@ int oracle_create(const paxisim_config* cfg, const paxisim_workload* wl,
   s->C = cfg->clusters;
   s->keep_xlog = cfg->clusters <= 16;
   s->OW = abd_ow(wl->outstanding);
+  s->NK = cfg->protocol == PAXISIM_WPAXOS ? cfg->keys : 1u;
+  s->q1 = cfg->q1;
+  s->q2 = cfg->q2;
+  if (cfg->protocol == PAXISIM_WPAXOS) {
+    /* kpaxos: Q1/Q2 from fz (wpaxos/kpaxos.go:15-27); no ReplyWhenCommit option
+     * (kpaxos.go:35-39) and the Paxos replica's -ephemeral_leader is not consulted */
+    s->q1 = cfg->fz ? PAXISIM_Q_FGRID_Q1 : PAXISIM_Q_GRID_ROW;
+    s->q2 = cfg->fz ? PAXISIM_Q_FGRID_Q2 : PAXISIM_Q_GRID_COLUMN;
+    s->cfg.reply_when_commit = 0;
+    s->cfg.ephemeral_leader = 0;
+  }
   s->cl = (cluster_t*)calloc(s->C, sizeof(cluster_t));
   if (!s->cl) { free(s); return fail(PAXISIM_ENOMEM, "oom clusters"); }
   for (i = 0; i < s->C; i++) {
     cluster_t* c = &s->cl[i];
-    entry_t* logs = (entry_t*)calloc((size_t)N * s->W, sizeof(entry_t));
+    entry_t* logs = (entry_t*)calloc((size_t)N * s->NK * s->W, sizeof(entry_t));
+    inst_t* insts = (inst_t*)calloc((size_t)N * s->NK, sizeof(inst_t));
     c->mbox = (rec_t*)malloc((size_t)s->D * N * s->NS * s->M * sizeof(rec_t));
     c->cnt = (uint8_t*)calloc((size_t)s->D * N * s->NS, 1);
-    if (!logs || !c->mbox || !c->cnt) { s->C = i + 1; oracle_destroy(s); return fail(PAXISIM_ENOMEM, "oom"); }
-    cluster_init(s, c, cfg->cluster_base + i, logs);
+    if (!logs || !insts || !c->mbox || !c->cnt) {
+      free(logs);
+      free(insts);
+      s->C = i;
+      free(c->mbox);
+      free(c->cnt);
+      oracle_destroy(s);
+      return fail(PAXISIM_ENOMEM, "oom");
+    }
+    cluster_init(s, c, cfg->cluster_base + i, logs, insts);
   }
   *out = s;
   return 0;
@@ -984,9 +1153,15 @@ int oracle_destroy(oracle_sim* s) {
   if (!s) return 0;
   for (i = 0; i < s->C; i++) {
     cluster_t* c = &s->cl[i];
-    if (c->rep[0].log) free(c->rep[0].log);
+    if (c->rep[0].inst) {
+      free(c->rep[0].inst[0].log);
+      for (r = 0; r < s->N; r++) {
+        uint32_t k;
+        for (k = 0; k < s->NK; k++) free(c->rep[r].inst[k].xlog);
+      }
+      free(c->rep[0].inst);
+    }
     for (r = 0; r < s->N; r++) {
-      free(c->rep[r].xlog);
       free(c->rep[r].kv_val);
       free(c->rep[r].ops);
       free(c->rep[r].hist);
@@ -1043,20 +1218,45 @@ int oracle_step(oracle_sim* s, uint32_t nsteps, int nthreads) {
   return 0;
 }
 
+static uint64_t expand_ballot(const struct oracle_sim* s, uint32_t b) {   /* to ballot.go:15-17 */
+  uint32_t rid = bal_id(b);
+  return b ? oracle_new_ballot(b >> 4, s->zone_of[rid], s->node_of[rid]) : 0;
+}
+
 static void fill_state(const struct oracle_sim* s, const cluster_t* c, uint32_t r,
                        paxisim_replica_state* o) {
   const replica_t* p = &c->rep[r];
-  uint32_t rid = bal_id(p->ballot);
+  const inst_t* q = &p->inst[0];
   memset(o, 0, sizeof *o);
-  o->ballot = p->ballot ? oracle_new_ballot(p->ballot >> 4, s->zone_of[rid], s->node_of[rid]) : 0;
-  o->slot = p->slot;
-  o->execute = p->execute;
-  o->active = p->active;
+  o->ballot = expand_ballot(s, q->ballot);
+  o->slot = q->slot;
+  o->execute = q->execute;
+  o->active = q->active;
   o->flags = p->flags;
-  o->digest = p->digest;
-  o->p1_acks = p->p1mask;
-  o->npending = p->npend;
+  o->digest = q->digest;
+  o->p1_acks = q->p1mask;
+  o->npending = q->npend;
   memcpy(o->delivered, p->delivered, sizeof o->delivered);
+  if (s->cfg.protocol == PAXISIM_WPAXOS) {   /* per-replica aggregate over the key instances */
+    uint32_t k, hi = 0;
+    uint64_t d = 0;
+    int32_t led = 0, ex = 0;
+    o->active = o->p1_acks = o->npending = 0;
+    for (k = 0; k < s->NK; k++) {
+      q = &p->inst[k];
+      if (q->ballot > hi) hi = q->ballot;
+      led += q->exists && (q->active || bal_id(q->ballot) == r);   /* Replica.keys() replica.go:110-118 */
+      ex += q->execute;
+      o->active += q->active;
+      o->p1_acks |= q->exists ? 1u << k : 0u;
+      o->npending += q->npend;
+      d = mix64(d ^ q->digest);
+    }
+    o->ballot = expand_ballot(s, hi);
+    o->slot = led;
+    o->execute = ex;
+    o->digest = d;
+  }
   if (s->cfg.protocol == PAXISIM_ABD) {            /* ABD: op counter, Done ops, KV digest, live ops */
     uint32_t k, live = 0;
     uint64_t d = 0;
@@ -1083,6 +1283,31 @@ int oracle_read_state(oracle_sim* s, uint64_t lo, uint64_t n, paxisim_replica_st
   if (lo + n > s->C) return fail(PAXISIM_ERANGE, "cluster range");
   for (i = 0; i < n; i++)
     for (r = 0; r < s->N; r++) fill_state(s, &s->cl[lo + i], r, &out[i * s->N + r]);
+  return 0;
+}
+
+int oracle_read_instances(oracle_sim* s, uint64_t lo, uint64_t n, paxisim_instance_state* out) {
+  uint64_t i;
+  uint32_t r, k;
+  if (!s || !out) return fail(PAXISIM_EINVAL, "null argument");
+  if (lo + n > s->C) return fail(PAXISIM_ERANGE, "cluster range");
+  for (i = 0; i < n; i++)
+    for (r = 0; r < s->N; r++)
+      for (k = 0; k < s->NK; k++) {
+        const inst_t* q = &s->cl[lo + i].rep[r].inst[k];
+        paxisim_instance_state* o = &out[(i * s->N + r) * s->NK + k];
+        memset(o, 0, sizeof *o);
+        o->ballot = expand_ballot(s, q->ballot);
+        o->slot = q->slot;
+        o->execute = q->execute;
+        o->active = q->active;
+        o->exists = q->exists;
+        o->p1_acks = q->p1mask;
+        o->npending = q->npend;
+        o->digest = q->digest;
+        o->policy_last = q->pol_last;
+        o->policy_hits = q->pol_hits;
+      }
   return 0;
 }
 
@@ -1123,14 +1348,16 @@ int oracle_check(oracle_sim* s, uint64_t* violations) {
   for (i = 0; i < s->C; i++) {
     const cluster_t* c = &s->cl[i];
     int bad = 0;
-    for (a = 0; a < s->N && !bad; a++)
-      for (b = a + 1; b < s->N && !bad; b++) {
-        const replica_t *p = &c->rep[a], *q = &c->rep[b];
-        if (p->execute == q->execute && p->digest != q->digest) bad = 1;
-        for (k = 0; k < CKR && !bad; k++)
-          for (j = 0; j < CKR && !bad; j++)
-            if (p->ck_e[k] && p->ck_e[k] == q->ck_e[j] && p->ck_d[k] != q->ck_d[j]) bad = 1;
-      }
+    uint32_t key;
+    for (key = 0; key < s->NK && !bad; key++)      /* per Paxos instance: WPaxos per key (tla Safety) */
+      for (a = 0; a < s->N && !bad; a++)
+        for (b = a + 1; b < s->N && !bad; b++) {
+          const inst_t *p = &c->rep[a].inst[key], *q = &c->rep[b].inst[key];
+          if (p->execute == q->execute && p->digest != q->digest) bad = 1;
+          for (k = 0; k < CKR && !bad; k++)
+            for (j = 0; j < CKR && !bad; j++)
+              if (p->ck_e[k] && p->ck_e[k] == q->ck_e[j] && p->ck_d[k] != q->ck_d[j]) bad = 1;
+        }
     v += (uint64_t)bad;
   }
   *violations = v;
@@ -1138,11 +1365,12 @@ int oracle_check(oracle_sim* s, uint64_t* violations) {
 }
 
 int oracle_exec_log(oracle_sim* s, uint64_t cl, uint32_t r, uint32_t* buf, uint32_t cap, uint32_t* n_out) {
-  const replica_t* p;
-  uint32_t n;
-  if (!s || !n_out || cl >= s->C || r >= s->N) return fail(PAXISIM_EINVAL, "bad argument");
+  const inst_t* p;
+  uint32_t n, key = r >> 16;                       /* WPaxos: replica | key << 16 */
+  r &= 0xFFFFu;
+  if (!s || !n_out || cl >= s->C || r >= s->N || key >= s->NK) return fail(PAXISIM_EINVAL, "bad argument");
   if (!s->keep_xlog) return fail(PAXISIM_EUNSUPP, "exec log kept only for <= 16 clusters");
-  p = &s->cl[cl].rep[r];
+  p = &s->cl[cl].rep[r].inst[key];
   n = p->nx < cap ? p->nx : cap;
   if (buf && n) memcpy(buf, p->xlog, n * sizeof(uint32_t));
   *n_out = p->nx;

@@ -30,8 +30,10 @@ int  oracle_step(oracle_sim* h, uint32_t nsteps, int nthreads);
 int  oracle_stats_get(oracle_sim* h, paxisim_stats* out);
 int  oracle_read_state(oracle_sim* h, uint64_t cluster_lo, uint64_t n,
                        paxisim_replica_state* out);
+int  oracle_read_instances(oracle_sim* h, uint64_t cluster_lo, uint64_t n,
+                           paxisim_instance_state* out);
 int  oracle_check(oracle_sim* h, uint64_t* violations);
-/* Executed command ids of (cluster, replica), in slot order (KAT support). */
+/* Executed command ids of (cluster, replica | key << 16), in slot order (KAT support). */
 int  oracle_exec_log(oracle_sim* h, uint64_t cluster, uint32_t replica,
                      uint32_t* buf, uint32_t cap, uint32_t* n_out);
 /* History.Linearizable over every (cluster, key) of the ABD op history. */

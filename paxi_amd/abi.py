@@ -6,7 +6,7 @@ structs, so the two speak exactly the same ABI.
 """
 import ctypes as C
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_N = 16
 MAX_ZONES = 16
 MAX_WORKERS = 32
@@ -114,6 +114,22 @@ class ReplicaState(C.Structure):
                 self.sent, self.dropped, self.discarded, self.commits, self.replies)
 
 
+class InstanceState(C.Structure):
+    """One Paxos instance: a Multi-Paxos replica's paxos.Paxos, or a WPaxos kpaxos per key."""
+    _fields_ = [
+        ("ballot", C.c_uint64),
+        ("slot", C.c_int32), ("execute", C.c_int32),
+        ("active", C.c_uint32), ("exists", C.c_uint32),
+        ("p1_acks", C.c_uint32), ("npending", C.c_uint32),
+        ("digest", C.c_uint64),
+        ("policy_last", C.c_uint32), ("policy_hits", C.c_uint32),
+    ]
+
+    def as_tuple(self):
+        return (self.ballot, self.slot, self.execute, self.active, self.exists, self.p1_acks,
+                self.npending, self.digest, self.policy_last, self.policy_hits)
+
+
 class Stats(C.Structure):
     _fields_ = [
         ("steps", C.c_uint64), ("clusters", C.c_uint64),
@@ -143,6 +159,7 @@ def declare(lib, prefix):
         "fault_add": (C.c_int, [h, P(Fault)]),
         "stats_get": (C.c_int, [h, P(Stats)]),
         "read_state": (C.c_int, [h, C.c_uint64, C.c_uint64, P(ReplicaState)]),
+        "read_instances": (C.c_int, [h, C.c_uint64, C.c_uint64, P(InstanceState)]),
         "check": (C.c_int, [h, P(C.c_uint64)]),
         "last_error": (C.c_char_p, []),
     }
@@ -196,3 +213,8 @@ def make_fault(kind, src, dst=ALL_DST, param=0, cluster_lo=0, cluster_hi=2**63, 
 
 def n_replicas(cfg):
     return sum(cfg.npz[i] for i in range(cfg.n_zones))
+
+
+def n_instances(cfg):
+    """Paxos instances per replica: one kpaxos per key for WPaxos, else one."""
+    return cfg.keys if cfg.protocol == WPAXOS else 1

@@ -16,6 +16,7 @@
 #include "lin_kernel.h"
 #include "paxisim_dev.h"
 #include "paxos_kernel.h"
+#include "wpaxos_kernel.h"
 
 using namespace pxs;
 
@@ -55,6 +56,13 @@ struct paxisim {
 
 static inline size_t rc_host(const Params& P, uint32_t r, uint64_t c) { return (size_t)r * P.C + c; }
 
+// compressed (n << 4) | r  ->  the 64-bit Ballot of ballot.go:15-17
+static uint64_t expand_ballot(const paxisim* h, uint32_t b) {
+  if (!b) return 0;
+  const uint32_t id = b & 15u;
+  return ((uint64_t)(b >> 4) << 32) | ((uint64_t)h->zone_of[id] << 16) | h->node_of[id];
+}
+
 extern "C" int paxisim_abi_version(void) { return PAXISIM_ABI_VERSION; }
 extern "C" const char* paxisim_last_error(void) { return g_err; }
 
@@ -70,6 +78,13 @@ __global__ void init_kernel(Params P) {
   reinterpret_cast<uint32_t*>(img + P.img.off_poison)[lane] = 0xFFFFFFFFu;
   if (P.protocol == PAXISIM_PAXOS)
     for (uint32_t r = 0; r < P.N; r++) P.slot[rc(P, r, c)] = 0xFFFFFFFFu;   // slot: -1 (paxos.go:45)
+  if (P.protocol == PAXISIM_WPAXOS)                                         // fresh kpaxos instances
+    for (uint32_t k = 0; k < P.keys; k++)
+      for (uint32_t r = 0; r < P.N; r++) {
+        const size_t si = (((size_t)blk * P.keys + k) * P.N + r) * LANES + lane;
+        P.wst[2 * si] = make_uint4(0u, 0xFFFFFFFFu, 0u, 0u);
+        P.wst[2 * si + 1] = make_uint4(0u, 0u, 0u, POL_NONE);
+      }
   if (c >= P.clusters) return;
   uint8_t* cnt = img + P.img.off_cnt;
   uint32_t* wcur = reinterpret_cast<uint32_t*>(img + P.img.off_wcur);
@@ -156,6 +171,65 @@ __global__ void gather_kernel(Params P, uint64_t lo, uint64_t n, paxisim_replica
     s.digest = d;
     s.npending = live;
   }
+  if (P.protocol == PAXISIM_WPAXOS) {   // aggregate over the key instances (paxisim.h read_state)
+    uint32_t hi = 0, led = 0, act = 0, ex = 0, np = 0, em = 0;
+    uint64_t d = 0;
+    for (uint32_t k = 0; k < P.keys; k++) {
+      const size_t si = (((c / LANES) * P.keys + k) * P.N + r) * LANES + (c % LANES);
+      const uint4 a = P.wst[2 * si], b = P.wst[2 * si + 1];
+      const uint32_t exists = (a.w >> 1) & 1u;
+      hi = a.x > hi ? a.x : hi;
+      led += exists && ((a.w & 1u) || bal_id(a.x) == r);    // Replica.keys() replica.go:110-118
+      act += a.w & 1u;
+      ex += a.z;
+      np += b.x;
+      em |= exists << k;
+      d = mix64(d ^ ((uint64_t)b.y | ((uint64_t)b.z << 32)));
+    }
+    s.ballot = hi;
+    s.slot = (int32_t)led;
+    s.execute = (int32_t)ex;
+    s.active = act;
+    s.p1_acks = em;
+    s.npending = np;
+    s.digest = d;
+  }
+  out[i] = s;
+}
+
+// read_instances: one record per (cluster, replica, instance)
+__global__ void gather_inst_kernel(Params P, uint64_t lo, uint64_t n, paxisim_instance_state* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * P.NI) return;
+  const uint64_t c = lo + i / P.NI;
+  const uint32_t r = (uint32_t)((i / P.NK) % P.N), k = (uint32_t)(i % P.NK);
+  paxisim_instance_state s;
+  memset(&s, 0, sizeof s);
+  if (P.protocol == PAXISIM_WPAXOS) {
+    const size_t si = (((c / LANES) * P.keys + k) * P.N + r) * LANES + (c % LANES);
+    const uint4 a = P.wst[2 * si], b = P.wst[2 * si + 1];
+    s.ballot = a.x;
+    s.slot = (int32_t)a.y;
+    s.execute = (int32_t)a.z;
+    s.active = a.w & 1u;
+    s.exists = (a.w >> 1) & 1u;
+    s.p1_acks = a.w >> 16;
+    s.npending = b.x;
+    s.digest = (uint64_t)b.y | ((uint64_t)b.z << 32);
+    s.policy_last = b.w & 0xFFu;
+    s.policy_hits = b.w >> 8;
+  } else {
+    const size_t j = rc(P, r, c);
+    s.ballot = P.ballot[j];
+    s.slot = (int32_t)P.slot[j];
+    s.execute = (int32_t)P.execute[j];
+    s.active = P.meta[j] & 1u;
+    s.exists = 1;
+    s.p1_acks = P.meta[j] >> 16;
+    s.npending = P.npend[j];
+    s.digest = P.digest[j];
+    s.policy_last = POL_NONE;
+  }
   out[i] = s;
 }
 
@@ -166,17 +240,34 @@ __global__ void check_kernel(Params P, uint64_t* out) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t bad = 0;
   if (c < P.clusters) {
-    for (uint32_t a = 0; a < P.N && !bad; a++)
-      for (uint32_t b = a + 1; b < P.N && !bad; b++) {
-        if (P.execute[rc(P, a, c)] == P.execute[rc(P, b, c)] && P.digest[rc(P, a, c)] != P.digest[rc(P, b, c)])
-          bad = 1;
-        for (uint32_t k = 0; k < CKR && !bad; k++) {
-          const uint32_t ea = P.ck_e[krc(P, k, a, c)];
-          if (!ea) continue;
-          for (uint32_t j = 0; j < CKR && !bad; j++)
-            if (P.ck_e[krc(P, j, b, c)] == ea && P.ck_d[krc(P, k, a, c)] != P.ck_d[krc(P, j, b, c)]) bad = 1;
-        }
+    auto exec_digest = [&](uint32_t key, uint32_t r, uint32_t& e, uint64_t& d) {
+      if (P.protocol == PAXISIM_WPAXOS) {
+        const size_t si = (((c / LANES) * P.keys + key) * P.N + r) * LANES + (c % LANES);
+        const uint4 a = P.wst[2 * si], b = P.wst[2 * si + 1];
+        e = a.z;
+        d = (uint64_t)b.y | ((uint64_t)b.z << 32);
+      } else {
+        e = P.execute[rc(P, r, c)];
+        d = P.digest[rc(P, r, c)];
       }
+    };
+    auto ck = [&](uint32_t k, uint32_t inst) { return ((size_t)k * P.NI + inst) * P.C + c; };
+    for (uint32_t key = 0; key < P.NK && !bad; key++)       // per Paxos instance (WPaxos: per key)
+      for (uint32_t a = 0; a < P.N && !bad; a++)
+        for (uint32_t b = a + 1; b < P.N && !bad; b++) {
+          uint32_t ea, eb;
+          uint64_t da, db;
+          exec_digest(key, a, ea, da);
+          exec_digest(key, b, eb, db);
+          if (ea == eb && da != db) bad = 1;
+          const uint32_t ia = key * P.N + a, ib = key * P.N + b;
+          for (uint32_t k = 0; k < CKR && !bad; k++) {
+            const uint32_t e = P.ck_e[ck(k, ia)];
+            if (!e) continue;
+            for (uint32_t j = 0; j < CKR && !bad; j++)
+              if (P.ck_e[ck(j, ib)] == e && P.ck_d[ck(k, ia)] != P.ck_d[ck(j, ib)]) bad = 1;
+          }
+        }
   }
   bad = wave_sum(bad);
   if ((threadIdx.x & 63) == 0 && bad) atomicAdd((unsigned long long*)out, (unsigned long long)bad);
@@ -190,6 +281,7 @@ static Image proto_image(uint32_t protocol, uint32_t N, uint32_t W, uint32_t K, 
     const uint32_t kv = N * K * LANES * 4u;
     return image_layout(kv, kv, N * abd_ow(WK) * ABD_OPF * LANES * 4u, N, WK, D);
   }
+  if (protocol == PAXISIM_WPAXOS) return image_layout(0, 0, 0, N, WK, D);   // instance state in HBM
   const uint32_t logb = N * W * LANES * 4u;
   return image_layout(logb, logb, logb, N, WK, D);
 }
@@ -197,9 +289,11 @@ static Image proto_image(uint32_t protocol, uint32_t N, uint32_t W, uint32_t K, 
 static int check_config(const paxisim_config* cfg, const paxisim_workload* wl, const paxisim_fault_process* fp,
                         uint32_t* N_out) {
   uint32_t N = 0;
-  if (cfg->protocol != PAXISIM_PAXOS && cfg->protocol != PAXISIM_ABD)
-    return fail(PAXISIM_EUNSUPP, "protocol %u not built", cfg->protocol);
+  if (cfg->protocol > PAXISIM_WPAXOS) return fail(PAXISIM_EUNSUPP, "protocol %u not built", cfg->protocol);
   if (cfg->protocol == PAXISIM_ABD && (cfg->keys < 1 || cfg->keys > 64)) return fail(PAXISIM_EINVAL, "keys");
+  if (cfg->protocol == PAXISIM_WPAXOS && (cfg->keys < 1 || cfg->keys > 32))
+    return fail(PAXISIM_EINVAL, "WPaxos keys must be in [1,32]");
+  if (cfg->policy_threshold > 255) return fail(PAXISIM_EINVAL, "policy_threshold");
   if (cfg->n_zones < 1 || cfg->n_zones > PAXISIM_MAX_ZONES) return fail(PAXISIM_EINVAL, "n_zones");
   for (uint32_t z = 0; z < cfg->n_zones; z++) {
     if (cfg->npz[z] < 1) return fail(PAXISIM_EINVAL, "npz[%u] must be >= 1", z);
@@ -287,6 +381,11 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
   P.Z = cfg->n_zones;
   P.keys = cfg->keys ? cfg->keys : 1;
   P.write_ppm = wl->write_ppm;
+  P.locality_ppm = wl->locality_ppm;
+  P.NK = cfg->protocol == PAXISIM_WPAXOS ? P.keys : 1u;
+  P.NI = P.NK * N;
+  P.adaptive = cfg->adaptive;
+  P.policy_thr = cfg->policy_threshold;
   P.H = cfg->protocol == PAXISIM_ABD ? cfg->history : 0;
   P.OW = abd_ow(wl->outstanding);
   P.W = cfg->window;
@@ -306,6 +405,14 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
   P.thrifty = cfg->thrifty;
   P.ephemeral = cfg->ephemeral_leader;
   P.rwc = cfg->reply_when_commit;
+  if (cfg->protocol == PAXISIM_WPAXOS) {
+    // kpaxos: Q1/Q2 from fz (wpaxos/kpaxos.go:15-27); no ReplyWhenCommit option
+    // (kpaxos.go:35-39); the Paxos replica's -ephemeral_leader is not consulted
+    P.q1 = cfg->fz ? PAXISIM_Q_FGRID_Q1 : PAXISIM_Q_GRID_ROW;
+    P.q2 = cfg->fz ? PAXISIM_Q_FGRID_Q2 : PAXISIM_Q_GRID_COLUMN;
+    P.rwc = 0;
+    P.ephemeral = 0;
+  }
   P.max_delay = cfg->max_delay;
   P.drop_ppm = fp->drop_ppm;
   P.drop_len = fp->drop_len;
@@ -318,13 +425,15 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     P.npz[z] = cfg->npz[z];
     P.zmask[z] = ((1u << cfg->npz[z]) - 1u) << r;
     for (uint32_t k = 0; k < cfg->npz[z]; k++, r++) {
+      P.zone_of[r] = z;
       h->zone_of[r] = z + 1;
       h->node_of[r] = k + 1;
     }
   }
   for (uint32_t w = 0; w < PAXISIM_MAX_WORKERS; w++) P.target[w] = wl->target[w];
 
-  const size_t C = P.C, NC = (size_t)N * C, blocks = C / LANES;
+  const size_t C = P.C, NC = (size_t)N * C, NIC = (size_t)P.NI * C, blocks = C / LANES;
+  const bool wp = P.protocol == PAXISIM_WPAXOS;
   P.img = proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D);
   P.rec_per_block = P.D * N * P.NS * P.M * LANES;
   // size the arena (rec last: it is the only region not zeroed)
@@ -333,13 +442,17 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     uint32_t* s7 = carve<uint32_t>(p, NC * 7);
     uint64_t* dg = carve<uint64_t>(p, NC);
     uint32_t* kc = carve<uint32_t>(p, C);
-    uint32_t* pend = carve<uint32_t>(p, NC * PMAX);
+    uint32_t* pend = carve<uint32_t>(p, wp ? 0 : NC * PMAX);
     uint32_t* fwd = carve<uint32_t>(p, NC * FMAX);
     uint32_t* links = carve<uint32_t>(p, NC * N * 2);
-    uint32_t* cke = carve<uint32_t>(p, NC * CKR);
-    uint64_t* ckd = carve<uint64_t>(p, NC * CKR);
+    uint32_t* cke = carve<uint32_t>(p, NIC * CKR);
+    uint64_t* ckd = carve<uint64_t>(p, NIC * CKR);
+    uint4* gst = carve<uint4>(p, NIC);
     uint32_t* st = carve<uint32_t>(p, NC * NSTAT);
-    uint32_t* reqx = carve<uint32_t>(p, NC * P.W);
+    uint32_t* reqx = carve<uint32_t>(p, wp ? 0 : NC * P.W);
+    uint4* wst = carve<uint4>(p, wp ? NIC * 2 : 0);
+    uint32_t* wlog = carve<uint32_t>(p, wp ? NIC * P.W * 4 : 0);
+    uint32_t* wpend = carve<uint32_t>(p, wp ? NIC * PMAX : 0);
     uint4* hist = carve<uint4>(p, NC * P.H);
     uint8_t* image = carve<uint8_t>(p, blocks * P.img.bytes);
     char* zend = p;
@@ -350,6 +463,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
       P.digest = dg; P.kc = kc; P.pend = pend; P.fwd = fwd;
       P.link_drop = links; P.link_slow = links + NC * N;
       P.ck_e = cke; P.ck_d = ckd; P.stats = st; P.reqx = reqx; P.hist = hist; P.image = image; P.rec = rec;
+      P.wst = wst; P.wlog = wlog; P.wpend = wpend; P.gst = gst;
     }
     return std::make_pair((size_t)zend, (size_t)p);
   };
@@ -417,6 +531,12 @@ static hipError_t launch_steps(paxisim* h, uint32_t t0, uint32_t n) {
 }
 
 static hipError_t launch_any(paxisim* h, uint32_t t0, uint32_t n) {
+  if (h->P.protocol == PAXISIM_WPAXOS) {
+    switch (h->P.N) {
+      case 9: return launch_steps<9, WPaxosProto>(h, t0, n);
+      default: return launch_steps<0, WPaxosProto>(h, t0, n);
+    }
+  }
   if (h->P.protocol == PAXISIM_ABD) {
     switch (h->P.N) {
       case 3: return launch_steps<3, AbdProto>(h, t0, n);
@@ -518,13 +638,25 @@ extern "C" int paxisim_read_state(paxisim* h, uint64_t lo, uint64_t n, paxisim_r
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   (void)hipFree(d);
   if (e != hipSuccess) return fail(PAXISIM_EDEVICE, "read_state: %s", hipGetErrorString(e));
-  for (size_t i = 0; i < cnt; i++) {       // expand to the 64-bit Ballot of ballot.go:15-17
-    const uint32_t b = (uint32_t)out[i].ballot;
-    if (b) {
-      const uint32_t id = b & 15u;
-      out[i].ballot = ((uint64_t)(b >> 4) << 32) | ((uint64_t)h->zone_of[id] << 16) | h->node_of[id];
-    }
-  }
+  for (size_t i = 0; i < cnt; i++) out[i].ballot = expand_ballot(h, (uint32_t)out[i].ballot);
+  return 0;
+}
+
+extern "C" int paxisim_read_instances(paxisim* h, uint64_t lo, uint64_t n, paxisim_instance_state* out) {
+  if (!h || !out) return fail(PAXISIM_EINVAL, "null argument");
+  if (lo + n > h->cfg.clusters || lo + n < lo) return fail(PAXISIM_ERANGE, "cluster range");
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const size_t cnt = (size_t)n * h->P.NI;
+  paxisim_instance_state* d = nullptr;
+  HIPCHK(hipMalloc(&d, cnt * sizeof(paxisim_instance_state)));
+  gather_inst_kernel<<<(unsigned)((cnt + 255) / 256), 256, 0, h->stream>>>(h->P, lo, n, d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d, cnt * sizeof(paxisim_instance_state), hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(PAXISIM_EDEVICE, "read_instances: %s", hipGetErrorString(e));
+  for (size_t i = 0; i < cnt; i++) out[i].ballot = expand_ballot(h, (uint32_t)out[i].ballot);
   return 0;
 }
 

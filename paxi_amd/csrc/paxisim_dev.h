@@ -77,7 +77,9 @@ enum { ABD_FREE = 0, ABD_GET = 1, ABD_SET = 2, ABD_DONE = 3 };
 
 struct Params {
   uint32_t protocol, N, Z, W, M, D, NS, WK, max_requests;
-  uint32_t keys, write_ppm, H, OW;
+  uint32_t keys, write_ppm, locality_ppm, H, OW;
+  uint32_t NK, NI;       // Paxos instances per replica (WPaxos: keys, else 1); per cluster NI = NK*N
+  uint32_t adaptive, policy_thr;
   uint32_t wk_magic;     // floor((2^32-1)/WK): (x % WK) by multiply-high + one correction
   uint64_t C;            // allocated cluster lanes (multiple of 64)
   uint64_t clusters;     // live clusters
@@ -85,19 +87,27 @@ struct Params {
   uint32_t q1, q2, fz, thrifty, ephemeral, rwc, max_delay, nfaults;
   uint32_t drop_ppm, drop_len, slow_ppm, slow_len, slow_min, slow_max;
   uint32_t npz[PAXISIM_MAX_ZONES], zmask[PAXISIM_MAX_ZONES];
+  uint32_t zone_of[PAXISIM_MAX_N];   // 0-based zone of each replica
   uint32_t target[PAXISIM_MAX_WORKERS];
   Image img;
   uint32_t rec_per_block;  // D*N*NS*M*64
   const paxisim_fault* faults;
-  // replica scalars [r][C]
+  // Paxos instance scalars [NI][C] (Multi-Paxos: NI = N); node scalars flags/nfwd [N][C]
   uint32_t *ballot, *slot, *execute, *meta, *flags, *npend, *nfwd;
   uint64_t* digest;
   uint32_t* kc;          // [C] per-cluster PRNG key
-  uint32_t* pend;        // [PMAX][N][C]
+  uint32_t* pend;        // [PMAX][NI][C]
   uint32_t* fwd;         // [FMAX][N][C]
   uint32_t *link_drop, *link_slow;  // [dst][N][C]: drop_until; slow_until | delay << 28
-  uint32_t* ck_e;        // [CKR][N][C]
-  uint64_t* ck_d;        // [CKR][N][C]
+  uint32_t* ck_e;        // [CKR][NI][C]
+  uint64_t* ck_d;        // [CKR][NI][C]
+  uint4* gst;            // [NI][C] ghost-entry summary {slot lo, slot hi, ballot min, ballot max}
+  // WPaxos kpaxos instances, one 32-B state + a W-entry window + PMAX pending per
+  // (blk, key, r, lane): {ballot, slot, execute, active|exists<<1|p1acks<<16,
+  // npend, digest lo, digest hi, policy last|hits<<8}; entries {ballot, cmd|flags, acks, request}
+  uint4* wst;            // [blk][K][N][64][2]
+  uint32_t* wlog;        // [blk][K][N][64][W][4]
+  uint32_t* wpend;       // [blk][K][N][64][PMAX]
   uint32_t* stats;       // [NSTAT][N][C]
   uint32_t* reqx;        // [blk][N][W][64] request side table (Paxos)
   uint4* hist;           // [N][C][H] completed ABD ops {key|write<<31, value, start, end}
@@ -137,9 +147,11 @@ __device__ __forceinline__ uint32_t req_cid(uint32_t q) { return q & CMD_MASK; }
 __device__ __forceinline__ uint32_t req_origin(uint32_t q) { return q >> 27; }
 __device__ __forceinline__ uint32_t mkreq(uint32_t cid, uint32_t o) { return cid | (o << 27); }
 
-// ---- message records: {hdr = type | n << 8, ballot, slot, cid} ------------
+// ---- message records: {hdr = type | n << 8 | key << 16, ballot, slot, cid} --
+// n: P1b payload records (ABD: the key); key: the WPaxos kpaxos instance
 __device__ __forceinline__ uint32_t hdr_type(uint32_t h) { return h & 0xFFu; }
-__device__ __forceinline__ uint32_t hdr_n(uint32_t h) { return h >> 8; }
+__device__ __forceinline__ uint32_t hdr_n(uint32_t h) { return (h >> 8) & 0xFFu; }
+__device__ __forceinline__ uint32_t hdr_key(uint32_t h) { return h >> 16; }
 
 // ---- quorum predicates on an ack mask (quorum.go:55-119) -----------------
 __device__ __forceinline__ bool quorum_ok(const Params& P, uint32_t kind, uint32_t mask) {

@@ -20,7 +20,7 @@ struct Ent { uint32_t b, c, a; };
 
 template <int NT>
 __device__ __forceinline__ uint32_t eidx(const Params& P, const Rep<NT>& x, int32_t s) {
-  return ((x.r * P.W + ((uint32_t)s & (P.W - 1u))) << 6) | x.lane;
+  return x.e0 + ((uint32_t)s & (P.W - 1u)) * x.es;
 }
 template <int NT>
 __device__ __forceinline__ Ent eget(const Rep<NT>& x, uint32_t i) { return Ent{x.l_a[i], x.l_b[i], x.l_c[i]}; }
@@ -33,7 +33,7 @@ __device__ __forceinline__ void eput(Rep<NT>& x, uint32_t i, const Ent& e) {
 // request side table slot for LDS entry index i
 template <int NT>
 __device__ __forceinline__ uint32_t* reqx_at(const Params& P, const Rep<NT>& x, uint32_t i) {
-  return &P.reqx[(size_t)x.blk * (P.N * P.W * LANES) + i];
+  return &x.reqx[i];
 }
 template <int NT>
 __device__ __forceinline__ uint32_t ereq(const Params& P, const Rep<NT>& x, uint32_t i, uint32_t c) {
@@ -105,6 +105,38 @@ __device__ __forceinline__ void handle_reply(const Params& P, Rep<NT>& x, uint32
 // ---------------------------------------------------------------------------
 // Multi-Paxos handlers
 // ---------------------------------------------------------------------------
+// WOVF / GHOST: raised on the replica and remembered per instance
+template <int NT>
+__device__ __forceinline__ void raise_win(Rep<NT>& x, uint32_t f) {
+  x.flags |= f;
+  x.iflags |= f & (PAXISIM_F_WOVF | PAXISIM_F_GHOST);
+}
+
+// An entry Go would create or update below execute (a "ghost": update() or
+// HandleP2a on a slot already executed here) is not stored.  A ghost is inert
+// except to HandleP2b (paxos.go:270-310), which for m.Ballot >= e.ballot adopts
+// a higher ballot or, on m.Ballot == e.ballot owned by self, panics on the nil
+// quorum.  Per instance, a summary {slot lo, slot hi, ballot min, ballot max}
+// in HBM (rarely touched) keeps that observation detectable.
+template <int NT>
+__device__ __forceinline__ void ghost(const Params& P, Rep<NT>& x, int32_t s, uint32_t b) {
+  const size_t gi = (size_t)x.inst * P.C + x.c;
+  uint4 g = (x.iflags & PAXISIM_F_GHOST) ? P.gst[gi] : make_uint4(0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0u);
+  raise_win(x, PAXISIM_F_GHOST);
+  g.x = min(g.x, (uint32_t)s);
+  g.y = max(g.y, (uint32_t)s);
+  g.z = min(g.z, b);
+  g.w = max(g.w, b);
+  P.gst[gi] = g;
+}
+template <int NT>
+__device__ __forceinline__ bool ghost_observed(const Params& P, const Rep<NT>& x, int32_t ms, uint32_t mb) {
+  if (!(x.iflags & PAXISIM_F_GHOST)) return false;
+  const uint4 g = P.gst[(size_t)x.inst * P.C + x.c];
+  if ((uint32_t)ms < g.x || (uint32_t)ms > g.y || mb < g.z) return false;
+  return mb > x.ballot || (bal_id(mb) == x.r && mb <= g.w);
+}
+
 template <int NT>
 __device__ __forceinline__ bool in_window(const Params& P, const Rep<NT>& x, int32_t s) {
   return s >= x.execute && s < x.execute + (int32_t)P.W;
@@ -112,7 +144,7 @@ __device__ __forceinline__ bool in_window(const Params& P, const Rep<NT>& x, int
 
 template <int NT>
 __device__ __forceinline__ void paxos_forward(const Params& P, Rep<NT>& x) {     // paxos.go:371-376
-  for (uint32_t i = 0; i < x.npend; i++) node_forward<NT>(P, x, bal_id(x.ballot), P.pend[krc(P, i, x.r, x.c)]);
+  for (uint32_t i = 0; i < x.npend; i++) node_forward<NT>(P, x, bal_id(x.ballot), x.pend[(size_t)i * x.pstride]);
   x.npend = 0;
 }
 
@@ -122,7 +154,7 @@ __device__ __forceinline__ void paxos_p1a(const Params& P, Rep<NT>& x) {      //
   if ((x.ballot >> 4) + 1u >= (1u << 27)) x.flags |= PAXISIM_F_BALLOT_OVF | PAXISIM_F_UNFAITHFUL;
   x.ballot = bal_next(x.ballot, x.r);
   x.p1mask = 1u << x.r;
-  post_broadcast<NT>(P, x, PAXISIM_MSG_P1A, x.ballot, 0u, 0u);
+  post_broadcast<NT>(P, x, PAXISIM_MSG_P1A | x.ktag, x.ballot, 0u, 0u);
 }
 
 template <int NT>
@@ -134,7 +166,7 @@ __device__ __forceinline__ void paxos_p2a(const Params& P, Rep<NT>& x, uint32_t 
     const uint32_t c = eset_req<NT>(P, x, i, cid | EF_EXISTS | EF_QUORUM, req);
     eput<NT>(x, i, Ent{x.ballot, c, 1u << x.r});
   } else {
-    x.flags |= PAXISIM_F_WOVF | PAXISIM_F_UNFAITHFUL;
+    raise_win(x, PAXISIM_F_WOVF | PAXISIM_F_UNFAITHFUL);
   }
   if (P.thrifty) {                                   // MulticastQuorum(N/2+1) (socket.go:132-145), ring order
     const uint32_t N = nrep<NT>(P);
@@ -142,9 +174,9 @@ __device__ __forceinline__ void paxos_p2a(const Params& P, Rep<NT>& x, uint32_t 
     intent_flush<NT>(P, x);
 #pragma nounroll
     for (uint32_t i = 1; i < N && sent < N / 2 + 1; i++, sent++)
-      send1<NT>(P, x, (x.r + i) % N, PAXISIM_MSG_P2A, x.ballot, (uint32_t)x.slot, cid);
+      send1<NT>(P, x, (x.r + i) % N, PAXISIM_MSG_P2A | x.ktag, x.ballot, (uint32_t)x.slot, cid);
   } else {
-    post_broadcast<NT>(P, x, PAXISIM_MSG_P2A, x.ballot, (uint32_t)x.slot, cid);
+    post_broadcast<NT>(P, x, PAXISIM_MSG_P2A | x.ktag, x.ballot, (uint32_t)x.slot, cid);
   }
 }
 
@@ -152,7 +184,7 @@ template <int NT>
 __device__ __forceinline__ void paxos_handle_request(const Params& P, Rep<NT>& x, uint32_t req) {  // paxos.go:86-97
   if (!x.active) {
     if (x.npend == PMAX) x.flags |= PAXISIM_F_PEND_OVF | PAXISIM_F_UNFAITHFUL;
-    else P.pend[krc(P, x.npend++, x.r, x.c)] = req;
+    else x.pend[(size_t)x.npend++ * x.pstride] = req;
     if (bal_id(x.ballot) != x.r) paxos_p1a<NT>(P, x);
   } else {
     paxos_p2a<NT>(P, x, req);
@@ -172,7 +204,7 @@ __device__ __forceinline__ void paxos_exec(const Params& P, Rep<NT>& x) {     //
     const uint32_t i = eidx<NT>(P, x, x.execute);
     const uint32_t c = x.l_b[i];
     if ((c & (EF_EXISTS | EF_COMMIT)) != (EF_EXISTS | EF_COMMIT)) break;
-    if (x.flags & PAXISIM_F_WOVF) x.flags |= PAXISIM_F_UNFAITHFUL;
+    if (x.iflags & PAXISIM_F_WOVF) x.flags |= PAXISIM_F_UNFAITHFUL;
     const uint32_t cmd = c & CMD_MASK;
     if (c & (EF_REQSELF | EF_REQEXT)) request_reply<NT>(P, x, ereq<NT>(P, x, i, c), cmd);
     x.digest = mix64(x.digest ^ (((uint64_t)(uint32_t)x.execute << 32) | cmd));
@@ -180,8 +212,9 @@ __device__ __forceinline__ void paxos_exec(const Params& P, Rep<NT>& x) {     //
     x.execute++;
     if ((uint32_t)x.execute % CKI == 0) {
       const uint32_t k = ((uint32_t)x.execute / CKI) % CKR;
-      P.ck_e[krc(P, k, x.r, x.c)] = (uint32_t)x.execute;
-      P.ck_d[krc(P, k, x.r, x.c)] = x.digest;
+      const size_t ci = ((size_t)k * P.NI + x.inst) * P.C + x.c;
+      P.ck_e[ci] = (uint32_t)x.execute;
+      P.ck_d[ci] = x.digest;
     }
   }
 }
@@ -193,7 +226,7 @@ __device__ __forceinline__ void paxos_handle_p1a(const Params& P, Rep<NT>& x, ui
     x.active = 0;
     paxos_forward<NT>(P, x);
   }
-  if (x.flags & PAXISIM_F_WOVF) x.flags |= PAXISIM_F_UNFAITHFUL;
+  if (x.iflags & PAXISIM_F_WOVF) x.flags |= PAXISIM_F_UNFAITHFUL;
   int32_t hi = x.slot;
   if (hi > x.execute + (int32_t)P.W - 1) hi = x.execute + (int32_t)P.W - 1;
   uint32_t n = 0;
@@ -204,7 +237,7 @@ __device__ __forceinline__ void paxos_handle_p1a(const Params& P, Rep<NT>& x, ui
   uint32_t ri;
   intent_flush<NT>(P, x);                                                    // keep per-link order
   if (!send_begin<NT>(P, x, bal_id(mb), 1u + n, ri)) return;
-  x.rec[ri] = make_uint4(PAXISIM_MSG_P1B | (n << 8), x.ballot, 0u, 0u);
+  x.rec[ri] = make_uint4(PAXISIM_MSG_P1B | (n << 8) | x.ktag, x.ballot, 0u, 0u);
   for (int32_t s = x.execute; s <= hi; s++) {
     const Ent e = eget<NT>(x, eidx<NT>(P, x, s));
     if (!(e.c & EF_EXISTS) || (e.c & EF_COMMIT)) continue;
@@ -235,9 +268,9 @@ __device__ __forceinline__ void paxos_handle_p1b(const Params& P, Rep<NT>& x, ui
         eput<NT>(x, i, Ent{cb.y, cb.w | EF_EXISTS, 0u});                      // quorum nil
       }
     } else if (s < x.execute) {
-      x.flags |= PAXISIM_F_GHOST;
+      ghost<NT>(P, x, s, cb.y);
     } else {
-      x.flags |= PAXISIM_F_WOVF;
+      raise_win(x, PAXISIM_F_WOVF);
     }
   }
   if (mb > x.ballot) {
@@ -249,7 +282,7 @@ __device__ __forceinline__ void paxos_handle_p1b(const Params& P, Rep<NT>& x, ui
     x.p1mask |= 1u << src;
     if (quorum_ok(P, P.q1, x.p1mask)) {
       x.active = 1;
-      if (x.flags & PAXISIM_F_WOVF) x.flags |= PAXISIM_F_UNFAITHFUL;
+      if (x.iflags & PAXISIM_F_WOVF) x.flags |= PAXISIM_F_UNFAITHFUL;
       int32_t hi = x.slot;
       if (hi > x.execute + (int32_t)P.W - 1) hi = x.execute + (int32_t)P.W - 1;
       for (int32_t s = x.execute; s <= hi; s++) {
@@ -259,11 +292,11 @@ __device__ __forceinline__ void paxos_handle_p1b(const Params& P, Rep<NT>& x, ui
         x.l_a[i] = x.ballot;
         x.l_b[i] = c | EF_QUORUM;
         x.l_c[i] = 1u << x.r;
-        post_broadcast<NT>(P, x, PAXISIM_MSG_P2A, x.ballot, (uint32_t)s, c & CMD_MASK);
+        post_broadcast<NT>(P, x, PAXISIM_MSG_P2A | x.ktag, x.ballot, (uint32_t)s, c & CMD_MASK);
       }
       const uint32_t np = x.npend;
       x.npend = 0;
-      for (uint32_t k = 0; k < np; k++) paxos_p2a<NT>(P, x, P.pend[krc(P, k, x.r, x.c)]);
+      for (uint32_t k = 0; k < np; k++) paxos_p2a<NT>(P, x, x.pend[(size_t)k * x.pstride]);
     }
   }
 }
@@ -293,19 +326,19 @@ __device__ __forceinline__ void paxos_handle_p2a(const Params& P, Rep<NT>& x, ui
         eput<NT>(x, i, Ent{mb, mcid | EF_EXISTS, 0u});
       }
     } else if (ms < x.execute) {
-      x.flags |= PAXISIM_F_GHOST;
+      ghost<NT>(P, x, ms, mb);
     } else {
-      x.flags |= PAXISIM_F_WOVF;
+      raise_win(x, PAXISIM_F_WOVF);
     }
   }
-  post_unicast<NT>(P, x, bal_id(mb), PAXISIM_MSG_P2B, x.ballot, (uint32_t)ms, 0u);
+  post_unicast<NT>(P, x, bal_id(mb), PAXISIM_MSG_P2B | x.ktag, x.ballot, (uint32_t)ms, 0u);
 }
 
 template <int NT>
 __device__ __forceinline__ void paxos_handle_p2b(const Params& P, Rep<NT>& x, uint32_t src, uint32_t mb,
                                                  int32_t ms) {                // paxos.go:270-310
   if (!in_window<NT>(P, x, ms)) {
-    if ((ms < x.execute && (x.flags & PAXISIM_F_GHOST)) || (ms >= x.execute && (x.flags & PAXISIM_F_WOVF)))
+    if (ms < x.execute ? ghost_observed<NT>(P, x, ms, mb) : (x.iflags & PAXISIM_F_WOVF) != 0)
       x.flags |= PAXISIM_F_UNFAITHFUL;
     return;
   }
@@ -328,7 +361,7 @@ __device__ __forceinline__ void paxos_handle_p2b(const Params& P, Rep<NT>& x, ui
     if (quorum_ok(P, P.q2, ack)) {
       x.l_b[i] = c | EF_COMMIT;
       x.commits++;
-      post_broadcast<NT>(P, x, PAXISIM_MSG_P3, mb, (uint32_t)ms, c & CMD_MASK);
+      post_broadcast<NT>(P, x, PAXISIM_MSG_P3 | x.ktag, mb, (uint32_t)ms, c & CMD_MASK);
       if (P.rwc) {
         const uint32_t q = ereq<NT>(P, x, i, c);
         if (!q) { x.flags |= PAXISIM_F_POISON; x.stop = true; return; }   // nil r.Reply
@@ -367,9 +400,9 @@ __device__ __forceinline__ void paxos_handle_p3(const Params& P, Rep<NT>& x, uin
       return;
     }
   } else if (ms < x.execute) {
-    x.flags |= PAXISIM_F_GHOST;
+    raise_win(x, PAXISIM_F_GHOST);
   } else {
-    x.flags |= PAXISIM_F_WOVF;
+    raise_win(x, PAXISIM_F_WOVF);
   }
   if (!P.rwc) paxos_exec<NT>(P, x);
 }
@@ -390,6 +423,15 @@ struct PaxosProto {
     x.npend = P.npend[i];
     x.nfwd = P.nfwd[i];
     x.digest = P.digest[i];
+    // the replica's one instance: LDS log window [r][W][lane], SoA pending table
+    x.iflags = x.flags & (PAXISIM_F_WOVF | PAXISIM_F_GHOST);
+    x.inst = x.r;
+    x.ktag = 0;
+    x.e0 = ((x.r * P.W) << 6) | x.lane;
+    x.es = LANES;
+    x.reqx = P.reqx + (size_t)x.blk * (P.N * P.W * LANES);
+    x.pend = P.pend + i;
+    x.pstride = P.NI * (uint32_t)P.C;
   }
   template <int NT>
   __device__ static __forceinline__ void store(const Params& P, const Rep<NT>& x) {

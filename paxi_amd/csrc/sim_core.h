@@ -25,6 +25,15 @@ struct Rep {
   int32_t slot, execute;
   uint32_t active, p1mask, flags, npend, nfwd;
   uint64_t digest;
+  // the bound Paxos instance (Multi-Paxos: the replica's one; WPaxos: one kpaxos per key)
+  uint32_t inst;                        // instance index in [NI] tables (key * N + r)
+  uint32_t ktag;                        // WPaxos: key << 16, tagged onto P1a..P3 records
+  uint32_t key, exists, pol;            // WPaxos: key, r.paxi[key] != nil, policy last | hits << 8
+  uint32_t iflags;                      // WOVF / GHOST of the bound instance
+  uint32_t e0, es;                      // log entry i of slot s: e0 + (s & (W-1)) * es
+  uint32_t* reqx;                       // request side table, indexed like the log
+  uint32_t* pend;                       // pending request k at pend[k * pstride]
+  uint32_t pstride;
   uint32_t du[NL], su[NL];              // link fault state: drop_until; slow_until | delay << 28
   uint32_t dv[PAXISIM_NMSG];            // delivered by type (constant-indexed only)
   uint32_t client, sent, dropped, discarded, commits, replies;
@@ -209,7 +218,20 @@ __device__ __forceinline__ void post_broadcast(const Params& P, Rep<NT>& x, uint
 // workload (benchmark.go:202-275): key and read/write of command cid
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t wl_hash(uint32_t kc, uint32_t cid) { return fmix32(fmix32(kc ^ 0x5BD1E995u) ^ cid); }
-__device__ __forceinline__ uint32_t wl_key(const Params& P, uint32_t kc, uint32_t cid) { return wl_hash(kc, cid) % P.keys; }
+// With locality (WPaxos per-zone clients, benchmark.go:202-213 "conflict"/Min):
+// worker w's command is, with P = locality, one of the keys k = z (mod Z) of
+// the zone z of its target replica, otherwise uniform over all keys.
+__device__ __forceinline__ uint32_t wl_key(const Params& P, uint32_t kc, uint32_t cid) {
+  const uint32_t h = wl_hash(kc, cid);
+  if (P.locality_ppm) {
+    uint32_t w = (cid - 1u) - P.WK * __umulhi(cid - 1u, P.wk_magic);   // (cid-1) % WK
+    if (w >= P.WK) w -= P.WK;
+    const uint32_t z = P.zone_of[P.target[w]];
+    const uint32_t nk = z < P.keys ? (P.keys - z + P.Z - 1u) / P.Z : 0u;
+    if (nk && ppm_hit(fmix32(h ^ 0x165667B1u), P.locality_ppm)) return z + P.Z * (h % nk);
+  }
+  return h % P.keys;
+}
 __device__ __forceinline__ bool wl_write(const Params& P, uint32_t kc, uint32_t cid) {
   return ppm_hit(fmix32(wl_hash(kc, cid) ^ 0x27D4EB2Fu), P.write_ppm);
 }

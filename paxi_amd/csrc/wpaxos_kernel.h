@@ -1,0 +1,186 @@
+// wpaxos_kernel.h — WPaxos handlers on gfx950 (a protocol policy of sim_core.h).
+//
+// Follows wpaxos/replica.go:42-108 and wpaxos/kpaxos.go:15-74 (cited per
+// function).  A WPaxos replica holds one paxos.Paxos ("kpaxos") per key,
+// created on first use (Replica.init, replica.go:36-40), with Q1/Q2 =
+// GridRow/GridColumn (fz = 0) or FGridQ1/Q2(fz) (kpaxos.go:15-27).  The kpaxos
+// Broadcast/Send wrappers (kpaxos.go:51-74) tag P1a..P3 with the key; here the
+// tag rides in the record header (x.ktag = key << 16).  Leaders migrate by the
+// consecutive policy (policy.go:49-69): after `threshold` consecutive requests
+// forwarded by one node of another zone, the leader sends that node a
+// LeaderChange and it steals the key with a phase-1 (replica.go:101-108).
+//
+// The Paxos handlers are paxos_kernel.h's, run on the bound instance: a
+// dispatch loads the key's instance registers from HBM, runs the handler and
+// writes them back.  Instance state of 64 clusters x 9 replicas x K keys does
+// not fit a workgroup's LDS, so it stays in HBM, laid out per (block, key,
+// replica, lane) so that one lane's state, window and pending list are each
+// contiguous:
+//   wst   [blk][K][N][64] x 32 B  {ballot, slot, execute, active|exists<<1|wovf,ghost<<2|p1acks<<16,
+//                                   npend, digest, policy last|hits<<8}
+//   wlog  [blk][K][N][64][W] x 16 B {ballot, cmd|flags, acks, request}
+//   wpend [blk][K][N][64][PMAX] x 4 B
+#pragma once
+#include "paxos_kernel.h"
+
+namespace pxs {
+
+constexpr uint32_t POL_NONE = 0xFFu;   // consecutive.last == "" (policy.go:50)
+
+template <int NT>
+__device__ __forceinline__ size_t wp_slot(const Params& P, const Rep<NT>& x, uint32_t key) {
+  return (((size_t)x.blk * P.keys + key) * nrep<NT>(P) + x.r) * LANES + x.lane;
+}
+
+// bind the kpaxos of `key`: its registers from HBM, its window and pending list
+template <int NT>
+__device__ __forceinline__ void wp_bind(const Params& P, Rep<NT>& x, uint32_t key) {
+  const size_t si = wp_slot<NT>(P, x, key);
+  const uint4 a = P.wst[2 * si], b = P.wst[2 * si + 1];
+  x.key = key;
+  x.ktag = key << 16;
+  x.inst = key * nrep<NT>(P) + x.r;
+  x.ballot = a.x;
+  x.slot = (int32_t)a.y;
+  x.execute = (int32_t)a.z;
+  x.active = a.w & 1u;
+  x.exists = (a.w >> 1) & 1u;
+  x.iflags = (a.w >> 2) & (PAXISIM_F_WOVF | PAXISIM_F_GHOST);
+  x.p1mask = a.w >> 16;
+  x.npend = b.x;
+  x.digest = (uint64_t)b.y | ((uint64_t)b.z << 32);
+  x.pol = b.w;
+  uint32_t* lb = P.wlog + si * P.W * 4u;
+  x.l_a = lb;
+  x.l_b = lb + 1;
+  x.l_c = lb + 2;
+  x.reqx = lb + 3;
+  x.pend = P.wpend + si * PMAX;
+}
+template <int NT>
+__device__ __forceinline__ void wp_unbind(const Params& P, const Rep<NT>& x) {
+  const size_t si = wp_slot<NT>(P, x, x.key);
+  P.wst[2 * si] = make_uint4(x.ballot, (uint32_t)x.slot, (uint32_t)x.execute,
+                             (x.active & 1u) | (x.exists << 1) | (x.iflags << 2) | (x.p1mask << 16));
+  P.wst[2 * si + 1] = make_uint4(x.npend, (uint32_t)x.digest, (uint32_t)(x.digest >> 32), x.pol);
+}
+
+// r.paxi[m.Key] without a prior init: a nil *kpaxos, whose use panics in Go
+template <int NT>
+__device__ __forceinline__ bool wp_get(Rep<NT>& x) {
+  if (x.exists) return true;
+  x.flags |= PAXISIM_F_POISON;
+  x.stop = true;
+  return false;
+}
+
+// consecutive.Hit (policy.go:55-69); threshold 0 is the null policy (policy.go:18-21)
+template <int NT>
+__device__ __forceinline__ uint32_t policy_hit(const Params& P, Rep<NT>& x, uint32_t id) {
+  if (P.policy_thr == 0) return POL_NONE;
+  uint32_t last = x.pol & 0xFFu, hits = x.pol >> 8;
+  if (id == last) {
+    hits++;
+  } else {
+    last = id;
+    hits = 1;
+  }
+  uint32_t res = POL_NONE;
+  if (hits >= P.policy_thr) {
+    res = last;
+    last = POL_NONE;
+    hits = 0;
+  }
+  x.pol = last | (hits << 8);
+  return res;
+}
+
+template <int NT>
+__device__ __forceinline__ void wp_handle_request(const Params& P, Rep<NT>& x, uint32_t req) {  // replica.go:42-66
+  x.exists = 1;                                                        // r.init(key)
+  if (!P.adaptive) {
+    paxos_handle_request<NT>(P, x, req);
+    return;
+  }
+  if (x.active || bal_id(x.ballot) == x.r || x.ballot == 0) {        // p.IsLeader() || p.Ballot() == 0
+    paxos_handle_request<NT>(P, x, req);
+    // m.NodeID: the receiving node for an HTTP request (http.go:96), the forwarder otherwise (node.go:167)
+    const uint32_t o = req_origin(req);
+    const uint32_t to = policy_hit<NT>(P, x, o == PAXISIM_CLIENT_SRC ? x.r : o);
+    if (to != POL_NONE && P.zone_of[to] != P.zone_of[x.r])            // LeaderChange{Key, To, From, Ballot}
+      post_unicast<NT>(P, x, to, PAXISIM_MSG_LEADERCHG | x.ktag, x.ballot, to, x.r);
+  } else {
+    node_forward<NT>(P, x, bal_id(x.ballot), req);                     // `go r.Forward(p.Leader(), m)`
+  }
+}
+
+struct WPaxosProto {
+  template <int NT>
+  __device__ static __forceinline__ void load(const Params& P, Rep<NT>& x) {
+    x.nfwd = P.nfwd[rc(P, x.r, x.c)];
+    x.e0 = 0;                        // entry of slot s: word 4*(s & (W-1)) of the lane's window
+    x.es = 4;
+    x.pstride = 1;
+    x.key = 0;
+    x.ktag = 0;
+  }
+  template <int NT>
+  __device__ static __forceinline__ void store(const Params& P, const Rep<NT>& x) {
+    P.nfwd[rc(P, x.r, x.c)] = x.nfwd;
+  }
+  template <int NT>
+  __device__ static __forceinline__ void client_request(const Params& P, Rep<NT>& x, uint32_t cid) {
+    wp_bind<NT>(P, x, wl_key(P, x.kc, cid));
+    wp_handle_request<NT>(P, x, mkreq(cid, PAXISIM_CLIENT_SRC));
+    wp_unbind<NT>(P, x);
+  }
+  // registrations replica.go:25-32
+  template <int NT>
+  __device__ static __forceinline__ void dispatch(const Params& P, Rep<NT>& x, uint32_t src, const uint4& m,
+                                                  uint32_t ri) {
+    const uint32_t type = hdr_type(m.x);
+    if (type == PAXISIM_MSG_REPLY) {                                   // node.recv (node.go:83-90)
+      x.dv[PAXISIM_MSG_REPLY]++;
+      handle_reply<NT>(P, x, m.w);
+      return;
+    }
+    wp_bind<NT>(P, x, type == PAXISIM_MSG_REQUEST ? wl_key(P, x.kc, m.w) : hdr_key(m.x));
+    switch (type) {
+      case PAXISIM_MSG_REQUEST:
+        x.dv[PAXISIM_MSG_REQUEST]++;
+        wp_handle_request<NT>(P, x, mkreq(m.w, src));
+        break;
+      case PAXISIM_MSG_P1A:                                            // handlePrepare 72-76
+        x.dv[PAXISIM_MSG_P1A]++;
+        x.exists = 1;
+        paxos_handle_p1a<NT>(P, x, m.y);
+        break;
+      case PAXISIM_MSG_P1B:                                            // handlePromise 78-82
+        x.dv[PAXISIM_MSG_P1B]++;
+        if (wp_get<NT>(x)) paxos_handle_p1b<NT>(P, x, src, m.y, ri, hdr_n(m.x));
+        break;
+      case PAXISIM_MSG_P2A:                                            // handleAccept 84-88
+        x.dv[PAXISIM_MSG_P2A]++;
+        x.exists = 1;
+        paxos_handle_p2a<NT>(P, x, m.y, (int32_t)m.z, m.w);
+        break;
+      case PAXISIM_MSG_P2B:                                            // handleAccepted 90-93
+        x.dv[PAXISIM_MSG_P2B]++;
+        if (wp_get<NT>(x)) paxos_handle_p2b<NT>(P, x, src, m.y, (int32_t)m.z);
+        break;
+      case PAXISIM_MSG_P3:                                             // handleCommit 95-99
+        x.dv[PAXISIM_MSG_P3]++;
+        x.exists = 1;
+        paxos_handle_p3<NT>(P, x, m.y, (int32_t)m.z, m.w);
+        break;
+      case PAXISIM_MSG_LEADERCHG:                                      // handleLeaderChange 101-108
+        x.dv[PAXISIM_MSG_LEADERCHG]++;
+        if (wp_get<NT>(x) && m.y == x.ballot && m.z == x.r) paxos_p1a<NT>(P, x);
+        break;
+      default: break;
+    }
+    wp_unbind<NT>(P, x);
+  }
+};
+
+}  // namespace pxs

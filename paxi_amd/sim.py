@@ -53,7 +53,7 @@ def load_library():
 
 EXPORTED = ["paxisim_abi_version", "paxisim_last_error", "paxisim_create", "paxisim_destroy",
             "paxisim_fault_add", "paxisim_step", "paxisim_sync", "paxisim_stats_get",
-            "paxisim_read_state", "paxisim_check", "paxisim_kernel_time", "paxisim_device_bytes",
+            "paxisim_read_state", "paxisim_read_instances", "paxisim_check", "paxisim_kernel_time", "paxisim_device_bytes",
             "paxisim_linearizable", "paxisim_history"]
 
 
@@ -93,6 +93,13 @@ class Simulation:
         n = self.cfg.clusters - lo if n is None else n
         arr = (abi.ReplicaState * (n * self.N))()
         _check(load_library().paxisim_read_state(self.h, lo, n, arr))
+        return arr
+
+    def read_instances(self, lo=0, n=None):
+        """Per (cluster, replica, key) Paxos instance state (paxisim_read_instances)."""
+        n = self.cfg.clusters - lo if n is None else n
+        arr = (abi.InstanceState * (n * self.N * abi.n_instances(self.cfg)))()
+        _check(load_library().paxisim_read_instances(self.h, lo, n, arr))
         return arr
 
     def check(self):

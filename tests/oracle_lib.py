@@ -72,16 +72,23 @@ class OracleSim:
         _check(lib().oracle_read_state(self.h, lo, n, arr))
         return arr
 
+    def read_instances(self, lo=0, n=None):
+        n = self.cfg.clusters - lo if n is None else n
+        arr = (abi.InstanceState * (n * self.N * abi.n_instances(self.cfg)))()
+        _check(lib().oracle_read_instances(self.h, lo, n, arr))
+        return arr
+
     def check(self):
         v = C.c_uint64()
         _check(lib().oracle_check(self.h, C.byref(v)))
         return v.value
 
-    def exec_log(self, cluster, replica):
+    def exec_log(self, cluster, replica, key=0):
+        rk = replica | (key << 16)
         n = C.c_uint32()
-        _check(lib().oracle_exec_log(self.h, cluster, replica, None, 0, C.byref(n)))
+        _check(lib().oracle_exec_log(self.h, cluster, rk, None, 0, C.byref(n)))
         buf = (C.c_uint32 * max(1, n.value))()
-        _check(lib().oracle_exec_log(self.h, cluster, replica, buf, n.value, C.byref(n)))
+        _check(lib().oracle_exec_log(self.h, cluster, rk, buf, n.value, C.byref(n)))
         return list(buf[: n.value])
 
     def linearizable(self):
