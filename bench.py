@@ -31,7 +31,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # P2a() entry); phase-1 / request / reply records priced as a write + read (64).
 # ABD: Get 80, GetReply 144, Set 96, SetReply 128 (+64 per op for the coordinator).
 ALG_BYTES = {"P2a": 160, "P2b": 144, "P3": 192, "P1a": 64, "P1b": 64, "Request": 64, "Reply": 64,
-             "Get": 80, "GetReply": 144, "Set": 96, "SetReply": 128}
+             "Get": 80, "GetReply": 144, "Set": 96, "SetReply": 128, "LeaderChange": 64}
 ALG_BYTES_PER_COMMIT = 64
 
 METRIC = "sim messages delivered/sec + committed slots/sec, 1M Paxos clusters, 1-8 GPU"
@@ -77,6 +77,15 @@ def workload(cfg_id, clusters, base, device, args):
         return cfg, wl, None, faults, {
             "workload": "BASELINE config 4: FGrid 3x3 (fz=1) x 512K clusters/GPU, ephemeral leaders, "
                         f"leader 1.1 crashed at step {args.crash_step}", "replicas": 9, "outstanding": 4}
+    if cfg_id == 5:
+        cfg = abi.make_config(protocol=abi.WPAXOS, npz=[3, 3, 3], keys=8, fz=0, adaptive=1, policy_threshold=3,
+                              clusters=clusters, cluster_base=base, seed=42, window=args.window, mbox_cap=24,
+                              max_delay=0, steps_per_launch=args.sim_steps, device=device)
+        wl = abi.make_workload(outstanding=9, target=list(range(9)), locality_ppm=700_000)
+        return cfg, wl, None, [], {
+            "workload": "BASELINE config 5: WPaxos 3 zones x 3 nodes, 8 keys (kpaxos instances) per cluster, "
+                        "Grid Q1/Q2, consecutive policy (threshold 3) object stealing, 70% zone-local keys",
+            "replicas": 9, "keys": 8, "outstanding": 9}
     raise SystemExit(f"unknown config {cfg_id}")
 
 
@@ -119,7 +128,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=4)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4])
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
     ap.add_argument("--clusters", type=int, default=None, help="clusters per GPU (default: the config's)")
     ap.add_argument("--sim-steps", type=int, default=50, help="virtual steps per bench step (per launch)")
     ap.add_argument("--window", type=int, default=16)
@@ -131,7 +140,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     if args.clusters is None:
-        args.clusters = {2: 1 << 20, 3: 1 << 20, 4: 1 << 19}[args.config]
+        args.clusters = {2: 1 << 20, 3: 1 << 20, 4: 1 << 19, 5: 1 << 18}[args.config]
 
     import torch
     import torch.distributed as dist
@@ -184,7 +193,9 @@ def main():
     if rank == 0:
         avg_launch_ms = kms / max(1, launches)
         achieved = alg_bytes(d) / max(1, launches) / (avg_launch_ms / 1e3) / 1e9   # rank 0's kernel, GB/s
-        proto = "AbdProto" if args.config == 3 else "PaxosProto"
+        proto = {3: "AbdProto", 5: "WPaxosProto"}.get(args.config, "PaxosProto")
+        occ = sim.occupancy()
+        desc.update({"tiles_per_cu": occ[0], "lds_per_tile": occ[1], "staged_msgs": occ[2]})
         desc.update({"clusters_per_gpu": args.clusters, "sim_steps_per_step": args.sim_steps,
                      "window": args.window, "mbox_cap": cfg.mbox_cap, "parallelism": f"cluster-sharded x{world}"})
         out = {

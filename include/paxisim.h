@@ -263,6 +263,11 @@ int  paxisim_linearizable(paxisim* h, uint64_t* anomalies, uint64_t* ops, uint64
  * completion order (the canonical history order). */
 int  paxisim_history(paxisim* h, uint64_t cluster, uint32_t* buf, uint32_t cap_ops, uint32_t* n_out);
 
+/* 64-cluster tiles of the step kernel resident per CU (hipOccupancy x tiles
+ * per workgroup), LDS per tile, and messages staged into LDS per
+ * replica-step (any pointer but the first may be NULL). */
+int  paxisim_occupancy(paxisim* h, int* blocks_per_cu, uint32_t* lds_bytes, uint32_t* staged);
+
 /* Bytes of device memory held by the handle. */
 int  paxisim_device_bytes(paxisim* h, uint64_t* bytes);
 

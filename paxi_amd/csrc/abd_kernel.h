@@ -135,6 +135,7 @@ __device__ __forceinline__ void abd_handle_setreply(const Params& P, Rep<NT>& x,
 }
 
 struct AbdProto {
+  static constexpr uint32_t kind = PAXISIM_ABD;
   template <int NT>
   __device__ static __forceinline__ void load(const Params& P, Rep<NT>& x) {
     const size_t i = rc(P, x.r, x.c);
@@ -157,14 +158,14 @@ struct AbdProto {
                                                   uint32_t) {
     const uint32_t key = hdr_n(m.x);
     switch (hdr_type(m.x)) {
-      case PAXISIM_MSG_REQUEST: x.dv[PAXISIM_MSG_REQUEST]++; abd_handle_request<NT>(P, x, m.w); break;
-      case PAXISIM_MSG_GET: x.dv[PAXISIM_MSG_GET]++; abd_handle_get<NT>(P, x, src, key, m.y); break;
+      case PAXISIM_MSG_REQUEST: dv_inc<NT>(x, PAXISIM_MSG_REQUEST); abd_handle_request<NT>(P, x, m.w); break;
+      case PAXISIM_MSG_GET: dv_inc<NT>(x, PAXISIM_MSG_GET); abd_handle_get<NT>(P, x, src, key, m.y); break;
       case PAXISIM_MSG_GETREPLY:
-        x.dv[PAXISIM_MSG_GETREPLY]++;
+        dv_inc<NT>(x, PAXISIM_MSG_GETREPLY);
         abd_handle_getreply<NT>(P, x, src, key, m.y, m.z, m.w);
         break;
-      case PAXISIM_MSG_SET: x.dv[PAXISIM_MSG_SET]++; abd_handle_set<NT>(P, x, src, key, m.y, m.z, m.w); break;
-      case PAXISIM_MSG_SETREPLY: x.dv[PAXISIM_MSG_SETREPLY]++; abd_handle_setreply<NT>(P, x, src, key, m.y); break;
+      case PAXISIM_MSG_SET: dv_inc<NT>(x, PAXISIM_MSG_SET); abd_handle_set<NT>(P, x, src, key, m.y, m.z, m.w); break;
+      case PAXISIM_MSG_SETREPLY: dv_inc<NT>(x, PAXISIM_MSG_SETREPLY); abd_handle_setreply<NT>(P, x, src, key, m.y); break;
       default: break;
     }
   }

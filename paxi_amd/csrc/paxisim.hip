@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -354,6 +355,13 @@ extern "C" int paxisim_destroy(paxisim* h) {
   return 0;
 }
 
+static hipError_t kernel_vgprs(const paxisim* h, int* v, int* maxthr);
+// stage_built<NT, Proto>() (sim_core.h) for the instance launch_any picks
+static bool stage_built_host(uint32_t protocol, uint32_t N) {
+  if (protocol == PAXISIM_ABD) return N == 3 || N == 5;
+  return N == 9;
+}
+
 extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload* wl, const paxisim_fault_process* fp,
                               paxisim** out) {
   if (!cfg || !wl || !out) return fail(PAXISIM_EINVAL, "null argument");
@@ -374,6 +382,10 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
   h->wl = *wl;
   h->fp = *fp;
   h->S = cfg->steps_per_launch ? cfg->steps_per_launch : 32;
+  {   // per-type delivered counts are 16-bit in the kernel: at most NS*M messages per replica-step
+    const uint32_t smax = 65535u / ((N + 1u) * cfg->mbox_cap);
+    if (h->S > smax) h->S = smax;
+  }
   Params& P = h->P;
   memset(&P, 0, sizeof P);
   P.protocol = cfg->protocol;
@@ -396,7 +408,6 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
   P.wk_magic = 0xFFFFFFFFu / P.WK;
   P.max_requests = wl->max_requests;
   P.clusters = cfg->clusters;
-  P.C = (cfg->clusters + LANES - 1) / LANES * LANES;
   P.cluster_base = cfg->cluster_base;
   P.seed = cfg->seed;
   P.q1 = cfg->q1;
@@ -432,9 +443,33 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
   }
   for (uint32_t w = 0; w < PAXISIM_MAX_WORKERS; w++) P.target[w] = wl->target[w];
 
+  P.img = proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D);
+  {
+    // Cluster groups per workgroup (sim_core.h): as many 64-cluster tiles as
+    // the step kernel's registers leave wave slots for on every SIMD
+    // (ceil(G*N/4) <= waves per SIMD) and the LDS holds, at most 4.
+    int vgprs = 0, maxthr = 0;
+    if (kernel_vgprs(h, &vgprs, &maxthr) != hipSuccess || vgprs <= 0) vgprs = 512;
+    if (maxthr <= 0) maxthr = (int)(N * LANES);
+    const uint32_t alloc = ((uint32_t)vgprs + 7u) / 8u * 8u;
+    const uint32_t wps = alloc >= 512u ? 1u : (512u / alloc < 8u ? 512u / alloc : 8u);
+    uint32_t G = 1, gmax = 4;
+    if (const char* e = getenv("PAXISIM_GROUPS")) gmax = (uint32_t)atoi(e) ? (uint32_t)atoi(e) : 1u;   // tuning
+    for (uint32_t g = 2; g <= gmax; g++)
+      if ((g * N + 3u) / 4u <= wps && g * N * LANES <= (uint32_t)maxthr && g * P.img.bytes <= LDS_MAX) G = g;
+    P.G = G;
+    // LDS stage for the first J picks of every replica's step, from what the groups leave
+    uint32_t jmax = 16;
+    if (const char* e = getenv("PAXISIM_STAGE")) jmax = (uint32_t)atoi(e);   // tuning override
+    const uint32_t room = (LDS_MAX / G - P.img.bytes) / (N * LANES * 16u);
+    P.J = room < jmax ? room : jmax;
+    if (!stage_built_host(P.protocol, N)) P.J = 0;   // that instance has no staged loop
+    P.off_stage = P.img.bytes;
+    P.lds_bytes = P.img.bytes + P.J * N * LANES * 16u;
+  }
+  P.C = (cfg->clusters + LANES * P.G - 1) / (LANES * P.G) * (LANES * P.G);
   const size_t C = P.C, NC = (size_t)N * C, NIC = (size_t)P.NI * C, blocks = C / LANES;
   const bool wp = P.protocol == PAXISIM_WPAXOS;
-  P.img = proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D);
   P.rec_per_block = P.D * N * P.NS * P.M * LANES;
   // size the arena (rec last: it is the only region not zeroed)
   size_t zero_bytes = 0, total = 0;
@@ -518,19 +553,77 @@ extern "C" int paxisim_fault_add(paxisim* h, const paxisim_fault* f) {
 template <int NT, class Proto>
 static hipError_t launch_steps(paxisim* h, uint32_t t0, uint32_t n) {
   const Params& P = h->P;
-  const unsigned grid = (unsigned)(P.C / LANES);
-  static thread_local bool attr_set = false;
-  if (!attr_set) {
+  const unsigned grid = (unsigned)(P.C / (LANES * P.G));
+  // The dynamic-LDS ceiling is set to what this launch uses, not to the CU's
+  // 160 KB: the runtime sizes every workgroup's LDS allocation by it, and a
+  // 160 KB ceiling would hold each CU to one resident workgroup.
+  static thread_local int attr_bytes = -1;
+  const int lds = (int)(P.G * P.lds_bytes);
+  if (attr_bytes != lds) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sim_steps<NT, Proto>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
-    attr_set = true;
+    attr_bytes = lds;
   }
-  sim_steps<NT, Proto><<<grid, P.N * LANES, P.img.bytes, h->stream>>>(P, t0, n);
+  sim_steps<NT, Proto><<<grid, P.G * P.N * LANES, (size_t)lds, h->stream>>>(P, t0, n);
   return hipGetLastError();
 }
 
+// Workgroups of the step kernel resident per CU (diagnostic: hipOccupancy API).
+template <int NT, class Proto>
+static hipError_t occupancy(paxisim* h, int* blocks) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, reinterpret_cast<const void*>(&sim_steps<NT, Proto>),
+                                                      (int)(h->P.G * h->P.N * LANES),
+                                                      (size_t)h->P.G * h->P.lds_bytes);
+}
+// VGPRs of the step kernel (sizes the cluster groups per workgroup)
+template <int NT, class Proto>
+static hipError_t vgprs_of(int* v, int* maxthr) {
+  hipFuncAttributes a;
+  hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&sim_steps<NT, Proto>));
+  if (e == hipSuccess) {
+    *v = a.numRegs;
+    *maxthr = a.maxThreadsPerBlock;
+  }
+  return e;
+}
+static hipError_t kernel_vgprs(const paxisim* h, int* v, int* m) {
+#ifdef PXS_ONLY_PAXOS5
+  return vgprs_of<5, PaxosProto>(v, m);
+#else
+  const uint32_t N = h->P.N;
+  if (h->P.protocol == PAXISIM_WPAXOS) return N == 9 ? vgprs_of<9, WPaxosProto>(v, m) : vgprs_of<0, WPaxosProto>(v, m);
+  if (h->P.protocol == PAXISIM_ABD)
+    return N == 3 ? vgprs_of<3, AbdProto>(v, m) : N == 5 ? vgprs_of<5, AbdProto>(v, m) : vgprs_of<0, AbdProto>(v, m);
+  switch (N) {
+    case 3: return vgprs_of<3, PaxosProto>(v, m);
+    case 5: return vgprs_of<5, PaxosProto>(v, m);
+    case 9: return vgprs_of<9, PaxosProto>(v, m);
+    default: return vgprs_of<0, PaxosProto>(v, m);
+  }
+#endif
+}
+static hipError_t occupancy_any(paxisim* h, int* blocks) {
+#ifdef PXS_ONLY_PAXOS5
+  return occupancy<5, PaxosProto>(h, blocks);
+#else
+  if (h->P.protocol == PAXISIM_WPAXOS) return h->P.N == 9 ? occupancy<9, WPaxosProto>(h, blocks) : occupancy<0, WPaxosProto>(h, blocks);
+  if (h->P.protocol == PAXISIM_ABD)
+    return h->P.N == 3 ? occupancy<3, AbdProto>(h, blocks) : h->P.N == 5 ? occupancy<5, AbdProto>(h, blocks) : occupancy<0, AbdProto>(h, blocks);
+  switch (h->P.N) {
+    case 3: return occupancy<3, PaxosProto>(h, blocks);
+    case 5: return occupancy<5, PaxosProto>(h, blocks);
+    case 9: return occupancy<9, PaxosProto>(h, blocks);
+    default: return occupancy<0, PaxosProto>(h, blocks);
+  }
+#endif
+}
+
 static hipError_t launch_any(paxisim* h, uint32_t t0, uint32_t n) {
+#ifdef PXS_ONLY_PAXOS5   // tuning builds: the config-2 kernel only
+  if (h->P.protocol == PAXISIM_PAXOS && h->P.N == 5) return launch_steps<5, PaxosProto>(h, t0, n);
+  return hipErrorInvalidConfiguration;
+#else
   if (h->P.protocol == PAXISIM_WPAXOS) {
     switch (h->P.N) {
       case 9: return launch_steps<9, WPaxosProto>(h, t0, n);
@@ -550,6 +643,7 @@ static hipError_t launch_any(paxisim* h, uint32_t t0, uint32_t n) {
     case 9: return launch_steps<9, PaxosProto>(h, t0, n);
     default: return launch_steps<0, PaxosProto>(h, t0, n);
   }
+#endif
 }
 
 extern "C" int paxisim_step(paxisim* h, uint32_t nsteps) {
@@ -668,6 +762,16 @@ extern "C" int paxisim_check(paxisim* h, uint64_t* violations) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(violations, h->d_scratch, sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int paxisim_occupancy(paxisim* h, int* blocks_per_cu, uint32_t* lds_bytes, uint32_t* staged) {
+  if (!h || !blocks_per_cu) return fail(PAXISIM_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  HIPCHK(occupancy_any(h, blocks_per_cu));
+  *blocks_per_cu *= (int)h->P.G;    // 64-cluster tiles resident per CU
+  if (lds_bytes) *lds_bytes = h->P.lds_bytes;
+  if (staged) *staged = h->P.J;
   return 0;
 }
 

@@ -90,6 +90,9 @@ struct Params {
   uint32_t zone_of[PAXISIM_MAX_N];   // 0-based zone of each replica
   uint32_t target[PAXISIM_MAX_WORKERS];
   Image img;
+  uint32_t J, off_stage;   // LDS stage: J staged picks per replica at LDS byte off_stage ([r][J][64] x 16 B)
+  uint32_t lds_bytes;      // LDS per cluster group (16-B multiple): the image + the stage
+  uint32_t G;              // cluster groups (64-cluster tiles) per workgroup
   uint32_t rec_per_block;  // D*N*NS*M*64
   const paxisim_fault* faults;
   // Paxos instance scalars [NI][C] (Multi-Paxos: NI = N); node scalars flags/nfwd [N][C]
@@ -177,12 +180,44 @@ __device__ __forceinline__ bool quorum_ok(const Params& P, uint32_t kind, uint32
   return false;
 }
 
+// ---- loads retired on the spot ----------------------------------------------
+// vmcnt counts stores as well as loads, and the compiler's waitcnt pass merges
+// control-flow paths conservatively: a load left in flight in a rarely taken
+// branch makes it wait on vmcnt (and so on every record store issued since) at
+// the next join of the step loop.  Loads off the staged path are therefore
+// consumed where they are issued.
+__device__ __forceinline__ uint32_t ldg(const uint32_t* p) {
+  uint32_t v = *p;
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ uint64_t ldg(const uint64_t* p) {
+  uint64_t v = *p;
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ uint4 ldg(const uint4* p) {
+  uint4 v = *p;
+  asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+  return v;
+}
+
 // ---- scripted faults (uniform across the wave: scalar loads) -------------
 __device__ __forceinline__ bool scripted(const Params& P, uint32_t kind, uint64_t gid, uint32_t src,
                                          uint32_t dst, uint32_t t, uint32_t* param) {
   bool hit = false;
   for (uint32_t i = 0; i < P.nfaults; i++) {
-    const paxisim_fault f = P.faults[i];
+    paxisim_fault f;
+    {
+      const uint32_t* fw = reinterpret_cast<const uint32_t*>(&P.faults[i]);
+      const uint4 a = ldg(reinterpret_cast<const uint4*>(fw));
+      const uint4 b = ldg(reinterpret_cast<const uint4*>(fw + 4));
+      const uint32_t c0 = ldg(fw + 8), c1 = ldg(fw + 9);
+      f.kind = a.x; f.src = a.y; f.dst = a.z; f.param = a.w;
+      f.cluster_lo = (uint64_t)b.x | ((uint64_t)b.y << 32);
+      f.cluster_hi = (uint64_t)b.z | ((uint64_t)b.w << 32);
+      f.step_from = c0; f.step_to = c1;
+    }
     if (f.kind != kind || f.src != src) continue;
     if (kind != PAXISIM_FAULT_CRASH && f.dst != PAXISIM_ALL_DST && f.dst != dst) continue;
     if (gid < f.cluster_lo || gid >= f.cluster_hi) continue;

@@ -38,7 +38,7 @@ __device__ __forceinline__ uint32_t* reqx_at(const Params& P, const Rep<NT>& x, 
 template <int NT>
 __device__ __forceinline__ uint32_t ereq(const Params& P, const Rep<NT>& x, uint32_t i, uint32_t c) {
   if (c & EF_REQSELF) return mkreq(c & CMD_MASK, PAXISIM_CLIENT_SRC);
-  if (c & EF_REQEXT) return *reqx_at(P, x, i);
+  if (c & EF_REQEXT) return ldg(reqx_at(P, x, i));
   return 0u;
 }
 // attach request q to entry flags c (whose command is cmd)
@@ -76,7 +76,7 @@ __device__ __forceinline__ void node_forward(const Params& P, Rep<NT>& x, uint32
   const uint32_t cid = req_cid(req);
   uint32_t i = 0;
   for (; i < x.nfwd; i++)
-    if (req_cid(P.fwd[krc(P, i, x.r, x.c)]) == cid) break;
+    if (req_cid(ldg(&P.fwd[krc(P, i, x.r, x.c)])) == cid) break;
   if (i == x.nfwd) {
     if (x.nfwd == FMAX) x.flags |= PAXISIM_F_PEND_OVF | PAXISIM_F_UNFAITHFUL;
     else P.fwd[krc(P, x.nfwd++, x.r, x.c)] = req;
@@ -91,14 +91,14 @@ template <int NT>
 __device__ __forceinline__ void handle_reply(const Params& P, Rep<NT>& x, uint32_t cid) {
   uint32_t i = 0;
   for (; i < x.nfwd; i++)
-    if (req_cid(P.fwd[krc(P, i, x.r, x.c)]) == cid) break;
+    if (req_cid(ldg(&P.fwd[krc(P, i, x.r, x.c)])) == cid) break;
   if (i == x.nfwd) {
     x.flags |= PAXISIM_F_UNFAITHFUL;
     return;
   }
-  const uint32_t req = P.fwd[krc(P, i, x.r, x.c)];
+  const uint32_t req = ldg(&P.fwd[krc(P, i, x.r, x.c)]);
   x.nfwd--;
-  P.fwd[krc(P, i, x.r, x.c)] = P.fwd[krc(P, x.nfwd, x.r, x.c)];
+  P.fwd[krc(P, i, x.r, x.c)] = ldg(&P.fwd[krc(P, x.nfwd, x.r, x.c)]);
   request_reply<NT>(P, x, req, cid);
 }
 
@@ -121,7 +121,8 @@ __device__ __forceinline__ void raise_win(Rep<NT>& x, uint32_t f) {
 template <int NT>
 __device__ __forceinline__ void ghost(const Params& P, Rep<NT>& x, int32_t s, uint32_t b) {
   const size_t gi = (size_t)x.inst * P.C + x.c;
-  uint4 g = (x.iflags & PAXISIM_F_GHOST) ? P.gst[gi] : make_uint4(0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0u);
+  uint4 g = make_uint4(0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0u);
+  if (x.iflags & PAXISIM_F_GHOST) g = ldg(&P.gst[gi]);
   raise_win(x, PAXISIM_F_GHOST);
   g.x = min(g.x, (uint32_t)s);
   g.y = max(g.y, (uint32_t)s);
@@ -132,7 +133,7 @@ __device__ __forceinline__ void ghost(const Params& P, Rep<NT>& x, int32_t s, ui
 template <int NT>
 __device__ __forceinline__ bool ghost_observed(const Params& P, const Rep<NT>& x, int32_t ms, uint32_t mb) {
   if (!(x.iflags & PAXISIM_F_GHOST)) return false;
-  const uint4 g = P.gst[(size_t)x.inst * P.C + x.c];
+  const uint4 g = ldg(&P.gst[(size_t)x.inst * P.C + x.c]);
   if ((uint32_t)ms < g.x || (uint32_t)ms > g.y || mb < g.z) return false;
   return mb > x.ballot || (bal_id(mb) == x.r && mb <= g.w);
 }
@@ -144,7 +145,7 @@ __device__ __forceinline__ bool in_window(const Params& P, const Rep<NT>& x, int
 
 template <int NT>
 __device__ __forceinline__ void paxos_forward(const Params& P, Rep<NT>& x) {     // paxos.go:371-376
-  for (uint32_t i = 0; i < x.npend; i++) node_forward<NT>(P, x, bal_id(x.ballot), x.pend[(size_t)i * x.pstride]);
+  for (uint32_t i = 0; i < x.npend; i++) node_forward<NT>(P, x, bal_id(x.ballot), ldg(&x.pend[(size_t)i * x.pstride]));
   x.npend = 0;
 }
 
@@ -252,7 +253,7 @@ __device__ __forceinline__ void paxos_handle_p1b(const Params& P, Rep<NT>& x, ui
                                               uint32_t n) {                   // paxos.go:164-230
   if (mb < x.ballot || x.active) return;
   for (uint32_t k = 0; k < n; k++) {                                          // update(): 164-180
-    const uint4 cb = x.rec[ri0 + (k + 1u) * LANES];
+    const uint4 cb = ldg(&x.rec[ri0 + (k + 1u) * LANES]);
     const int32_t s = (int32_t)cb.z;
     if (s > x.slot) x.slot = s;
     if (in_window<NT>(P, x, s)) {
@@ -296,7 +297,7 @@ __device__ __forceinline__ void paxos_handle_p1b(const Params& P, Rep<NT>& x, ui
       }
       const uint32_t np = x.npend;
       x.npend = 0;
-      for (uint32_t k = 0; k < np; k++) paxos_p2a<NT>(P, x, x.pend[(size_t)k * x.pstride]);
+      for (uint32_t k = 0; k < np; k++) paxos_p2a<NT>(P, x, ldg(&x.pend[(size_t)k * x.pstride]));
     }
   }
 }
@@ -411,6 +412,7 @@ __device__ __forceinline__ void paxos_handle_p3(const Params& P, Rep<NT>& x, uin
 // protocol policy
 // ---------------------------------------------------------------------------
 struct PaxosProto {
+  static constexpr uint32_t kind = PAXISIM_PAXOS;
   template <int NT>
   __device__ static __forceinline__ void load(const Params& P, Rep<NT>& x) {
     const size_t i = rc(P, x.r, x.c);
@@ -453,13 +455,13 @@ struct PaxosProto {
   __device__ static __forceinline__ void dispatch(const Params& P, Rep<NT>& x, uint32_t src, const uint4& m,
                                                   uint32_t ri) {
     switch (hdr_type(m.x)) {
-      case PAXISIM_MSG_REQUEST: x.dv[PAXISIM_MSG_REQUEST]++; handle_request<NT>(P, x, mkreq(m.w, src)); break;
-      case PAXISIM_MSG_REPLY: x.dv[PAXISIM_MSG_REPLY]++; handle_reply<NT>(P, x, m.w); break;
-      case PAXISIM_MSG_P1A: x.dv[PAXISIM_MSG_P1A]++; paxos_handle_p1a<NT>(P, x, m.y); break;
-      case PAXISIM_MSG_P1B: x.dv[PAXISIM_MSG_P1B]++; paxos_handle_p1b<NT>(P, x, src, m.y, ri, hdr_n(m.x)); break;
-      case PAXISIM_MSG_P2A: x.dv[PAXISIM_MSG_P2A]++; paxos_handle_p2a<NT>(P, x, m.y, (int32_t)m.z, m.w); break;
-      case PAXISIM_MSG_P2B: x.dv[PAXISIM_MSG_P2B]++; paxos_handle_p2b<NT>(P, x, src, m.y, (int32_t)m.z); break;
-      case PAXISIM_MSG_P3: x.dv[PAXISIM_MSG_P3]++; paxos_handle_p3<NT>(P, x, m.y, (int32_t)m.z, m.w); break;
+      case PAXISIM_MSG_REQUEST: dv_inc<NT>(x, PAXISIM_MSG_REQUEST); handle_request<NT>(P, x, mkreq(m.w, src)); break;
+      case PAXISIM_MSG_REPLY: dv_inc<NT>(x, PAXISIM_MSG_REPLY); handle_reply<NT>(P, x, m.w); break;
+      case PAXISIM_MSG_P1A: dv_inc<NT>(x, PAXISIM_MSG_P1A); paxos_handle_p1a<NT>(P, x, m.y); break;
+      case PAXISIM_MSG_P1B: dv_inc<NT>(x, PAXISIM_MSG_P1B); paxos_handle_p1b<NT>(P, x, src, m.y, ri, hdr_n(m.x)); break;
+      case PAXISIM_MSG_P2A: dv_inc<NT>(x, PAXISIM_MSG_P2A); paxos_handle_p2a<NT>(P, x, m.y, (int32_t)m.z, m.w); break;
+      case PAXISIM_MSG_P2B: dv_inc<NT>(x, PAXISIM_MSG_P2B); paxos_handle_p2b<NT>(P, x, src, m.y, (int32_t)m.z); break;
+      case PAXISIM_MSG_P3: dv_inc<NT>(x, PAXISIM_MSG_P3); paxos_handle_p3<NT>(P, x, m.y, (int32_t)m.z, m.w); break;
       default: break;
     }
   }

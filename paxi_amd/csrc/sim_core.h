@@ -34,8 +34,7 @@ struct Rep {
   uint32_t* reqx;                       // request side table, indexed like the log
   uint32_t* pend;                       // pending request k at pend[k * pstride]
   uint32_t pstride;
-  uint32_t du[NL], su[NL];              // link fault state: drop_until; slow_until | delay << 28
-  uint32_t dv[PAXISIM_NMSG];            // delivered by type (constant-indexed only)
+  uint32_t dvp[PAXISIM_NMSG / 2];       // delivered by type, two 16-bit counts per word (constant-indexed)
   uint32_t client, sent, dropped, discarded, commits, replies;
   uint32_t send_seq;
   uint32_t dmask, fmask;                // per-step: dropped / flaky destinations
@@ -51,6 +50,19 @@ struct Rep {
 
 template <int NT>
 __device__ __forceinline__ uint32_t nrep(const Params& P) { return NT ? (uint32_t)NT : P.N; }
+
+// delivered-by-type counters: 16 bits each, two per register (a launch's
+// steps are capped so that no count can reach 2^16, paxisim.hip)
+template <int NT>
+__device__ __forceinline__ void dv_inc(Rep<NT>& x, uint32_t k) { x.dvp[k >> 1] += (k & 1u) ? 0x10000u : 1u; }
+template <int NT>
+__device__ __forceinline__ uint32_t dv_get(const Rep<NT>& x, uint32_t k) { return (x.dvp[k >> 1] >> ((k & 1u) * 16u)) & 0xFFFFu; }
+
+// A global load consumed on the spot.  vmcnt counts stores too, so a load
+// whose use lies behind a handler's record stores makes the compiler wait for
+// those stores; retiring the load inside its own branch keeps that wait off
+// the staged (LDS) path that merges with it.
+__device__ __forceinline__ uint4 load_now(const uint4* p) { return ldg(p); }
 
 // The empty asm keeps LLVM from folding a select chain back into an alloca +
 // dynamic index (which would put the register array in scratch memory).
@@ -99,7 +111,8 @@ __device__ __forceinline__ bool send_begin(const Params& P, Rep<NT>& x, uint32_t
 // Per step: fold crash / drop / slow / flaky of every outgoing link into masks
 // (the filter order crash -> drop -> flaky -> slow is kept by send_begin).
 template <int NT>
-__device__ __forceinline__ void link_masks(const Params& P, Rep<NT>& x) {
+__device__ __forceinline__ void link_masks(const Params& P, Rep<NT>& x, const uint32_t (&du)[Rep<NT>::NL],
+                                           const uint32_t (&su)[Rep<NT>::NL]) {
   const uint32_t N = nrep<NT>(P);
   uint32_t dm = 0, fm = 0;
   uint64_t dl = 0;
@@ -107,8 +120,8 @@ __device__ __forceinline__ void link_masks(const Params& P, Rep<NT>& x) {
   for (uint32_t d = 0; d < Rep<NT>::NL; d++) {
     if (d >= N) continue;
     uint32_t delay = 0;
-    bool drop = x.t < x.du[d];
-    if (x.t < (x.su[d] & (T_MAX - 1u))) delay = x.su[d] >> 28;
+    bool drop = x.t < du[d];
+    if (x.t < (su[d] & (T_MAX - 1u))) delay = su[d] >> 28;
     if (P.nfaults) {
       drop = drop || scripted(P, PAXISIM_FAULT_DROP, x.gid, x.r, d, x.t, nullptr);
       uint32_t p = 0;
@@ -275,18 +288,26 @@ __device__ __forceinline__ void client_reply(const Params& P, Rep<NT>& x, uint32
 // Random fault process: per idle outgoing link, one draw may open a drop and
 // / or a slow window.
 // ---------------------------------------------------------------------------
+// The link state {drop_until, slow_until | delay << 28} of every outgoing link
+// lives in HBM ([dst][N][C], lanes coalesced): loaded once per step, written
+// back when a window opens; it is not held in registers across the step.
 template <int NT>
-__device__ __forceinline__ void fault_process(const Params& P, Rep<NT>& x) {
+__device__ __forceinline__ void fault_process(const Params& P, Rep<NT>& x, uint32_t (&du)[Rep<NT>::NL],
+                                              uint32_t (&su)[Rep<NT>::NL]) {
   if (P.drop_ppm == 0 && P.slow_ppm == 0) return;
 #pragma unroll
   for (uint32_t d = 0; d < Rep<NT>::NL; d++) {
     if (d >= nrep<NT>(P) || d == x.r) continue;
     const uint32_t u = draw(x.hs, tag(PUR_LINK, x.r, d));
-    if (P.drop_ppm && x.t >= x.du[d] && ppm_hit16(u & 0xFFFFu, P.drop_ppm)) x.du[d] = x.t + P.drop_len;
-    if (P.slow_ppm && x.t >= (x.su[d] & (T_MAX - 1u)) && ppm_hit16(u >> 16, P.slow_ppm)) {
+    if (P.drop_ppm && x.t >= du[d] && ppm_hit16(u & 0xFFFFu, P.drop_ppm)) {
+      du[d] = x.t + P.drop_len;
+      P.link_drop[krc(P, d, x.r, x.c)] = du[d];
+    }
+    if (P.slow_ppm && x.t >= (su[d] & (T_MAX - 1u)) && ppm_hit16(u >> 16, P.slow_ppm)) {
       const uint32_t span = P.slow_max - P.slow_min + 1u;
       const uint32_t v = draw(x.hs, tag(PUR_SLOWD, x.r, d));
-      x.su[d] = (x.t + P.slow_len) | ((P.slow_min + __umulhi(v, span)) << 28);
+      su[d] = (x.t + P.slow_len) | ((P.slow_min + __umulhi(v, span)) << 28);
+      P.link_slow[krc(P, d, x.r, x.c)] = su[d];
     }
   }
 }
@@ -295,7 +316,7 @@ __device__ __forceinline__ void fault_process(const Params& P, Rep<NT>& x) {
 // One replica, one step
 // ---------------------------------------------------------------------------
 #ifdef PXS_STAMPS
-struct Stamps { unsigned long long setup, loop, barrier, trips, msgs, steps, pick, disp, wait, flush; };
+struct Stamps { unsigned long long setup, loop, barrier, trips, msgs, steps, pick, disp, wait, flush, stage, tail; };
 __device__ __forceinline__ unsigned long long stamp() {
   unsigned long long t;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -303,7 +324,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 }
 #endif
 
-template <int NT, class Proto>
+template <int NT, class Proto, bool STAGED>
 __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
 #ifdef PXS_STAMPS
                                              , void* stp
@@ -319,27 +340,40 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
   x.stop = false;
   x.im = 0;
   x.hs = step_key(x.kc, x.t);
-  fault_process<NT>(P, x);
-  x.crashed = P.nfaults && scripted(P, PAXISIM_FAULT_CRASH, x.gid, x.r, 0u, x.t, nullptr);
-  link_masks<NT>(P, x);
+  {
+    uint32_t du[Rep<NT>::NL], su[Rep<NT>::NL];
+#pragma unroll
+    for (uint32_t d = 0; d < Rep<NT>::NL; d++) {
+      du[d] = d < N ? P.link_drop[krc(P, d, x.r, x.c)] : 0u;
+      su[d] = d < N ? P.link_slow[krc(P, d, x.r, x.c)] : 0u;
+    }
+    fault_process<NT>(P, x, du, su);
+    x.crashed = P.nfaults && scripted(P, PAXISIM_FAULT_CRASH, x.gid, x.r, 0u, x.t, nullptr);
+    link_masks<NT>(P, x, du, su);
+  }
 
   const uint32_t box0 = (x.b0 * N + x.r) * NS;          // inbox boxes: box0 + src
-  uint32_t rem[NSMAX], pos[NSMAX], total = 0;
+  // per source: records left (rem) and the step's initial count, packed in
+  // bytes (c0w), so a source's FIFO position is c0 - rem without a register each
+  constexpr uint32_t NCW = (NSMAX + 3u) / 4u;
+  uint32_t rem[NSMAX], c0w[NCW], total = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < NCW; k++) c0w[k] = 0;
 #pragma unroll
   for (uint32_t s = 0; s < NSMAX; s++) {
     rem[s] = 0;
-    pos[s] = 0;
     if (s < NS) {
       uint32_t n = x.l_cnt[((box0 + s) << 6) | x.lane];
       if (x.crashed && s < N && n) {                    // socket.Recv discards (socket.go:111-118)
         for (uint32_t k = 0; k < n;) {
-          const uint32_t h = x.rec[(((box0 + s) * P.M + k) << 6) | x.lane].x;
+          const uint32_t h = ldg(&x.rec[(((box0 + s) * P.M + k) << 6) | x.lane]).x;
           x.discarded++;
           k += 1u + (hdr_type(h) == PAXISIM_MSG_P1B ? hdr_n(h) : 0u);
         }
         n = 0;
       }
       rem[s] = n;
+      c0w[s >> 2] |= n << ((s & 3u) * 8u);
       total += n;
     }
   }
@@ -357,49 +391,99 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
 #endif
   uint32_t u = 0, i = 0, src = 0, ri = 0;
   uint4 m = make_uint4(0u, 0u, 0u, 0u);
-  auto pick = [&](uint32_t idx, uint32_t& psrc, uint32_t& pri) {
-    if (!(idx & 1u)) u = draw(x.hs, tag(PUR_ORDER, x.r, idx >> 1));
-    uint32_t pk = (((idx & 1u) ? (u >> 16) : (u & 0xFFFFu)) * total) >> 16;
+  // pick idx: the source of the idx-th message, given the remaining counts
+  auto pick_from = [&](uint32_t idx, uint32_t tot, const uint32_t (&rm)[NSMAX], uint32_t& uu, uint32_t& psrc,
+                       uint32_t& pri) {
+    if (!(idx & 1u)) uu = draw(x.hs, tag(PUR_ORDER, x.r, idx >> 1));
+    uint32_t pk = (((idx & 1u) ? (uu >> 16) : (uu & 0xFFFFu)) * tot) >> 16;
     bool found = false;
     psrc = 0;
     uint32_t p0 = 0;
 #pragma unroll
     for (uint32_t s = 0; s < NSMAX; s++) {
-      const uint32_t rs = opaque(rem[s]);
+      const uint32_t rs = opaque(rm[s]);
       const bool here = !found && pk < rs;
-      if (here) { psrc = s; p0 = opaque(pos[s]); found = true; }
+      if (here) { psrc = s; p0 = ((c0w[s >> 2] >> ((s & 3u) * 8u)) & 0xFFu) - rs; found = true; }
       else if (!found) pk -= rs;
     }
     pri = (((box0 + psrc) * P.M + p0) << 6) | x.lane;
   };
+  auto pick = [&](uint32_t idx, uint32_t& psrc, uint32_t& pri) { pick_from(idx, total, rem, u, psrc, pri); };
+
+  // Stage the records of the first J picks into LDS before handling any: the
+  // merge order is a function of the counts alone while every message is one
+  // record, so the picks are known up front and their loads go out together
+  // (one global_load_lds per pick, straight to this wave's LDS stage rows)
+  // instead of one dependent HBM round trip per message.  A multi-record P1b
+  // changes the later picks: staged entries after it are dropped (jv).
+  uint32_t jv = 0;
+  const uint4* stage = nullptr;
+#ifdef PXS_STAMPS
+  const unsigned long long g0 = stamp();
+  unsigned long long fe = g0;
+#endif
+  if constexpr (STAGED) {
+    const uint32_t sbase = __builtin_amdgcn_readfirstlane(P.off_stage + x.r * P.J * 1024u);
+    stage = reinterpret_cast<const uint4*>(x.l_cnt - P.img.off_cnt + sbase) + x.lane;
+    uint32_t srem[NSMAX], su = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < NSMAX; s++) srem[s] = rem[s];
+    for (uint32_t j = 0; j < P.J; j++) {
+      if (!__ballot(j < total)) break;
+      if (j < total) {
+        uint32_t ssrc, sri;
+        pick_from(j, total - j, srem, su, ssrc, sri);
+#pragma unroll
+        for (uint32_t s = 0; s < NSMAX; s++) srem[s] = opaque(srem[s]) - (s == ssrc ? 1u : 0u);
+        __builtin_amdgcn_global_load_lds(
+            (__attribute__((address_space(1))) void*)(x.rec + sri),
+            (__attribute__((address_space(3))) void*)((__attribute__((address_space(3))) uint8_t*)(x.l_cnt -
+                                                      P.img.off_cnt) + sbase + j * 1024u),
+            16, 0, 0);
+      }
+    }
+    jv = total < P.J ? total : P.J;
+    // vmcnt(0) (gfx9 encoding: expcnt, lgkmcnt at max) as a builtin, so the
+    // compiler's waitcnt pass knows the stage is complete and does not re-wait
+    // (behind this step's record stores) before every stage read
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+  }
+#ifdef PXS_STAMPS
+  st.stage += stamp() - g0;
+#endif
   if (total) {
     pick(0, src, ri);
-    m = x.rec[ri];
+    if constexpr (STAGED) {
+      if (jv) m = stage[0];
+      else m = load_now(x.rec + ri);
+    } else {
+      m = x.rec[ri];
+    }
   }
   while (total && !x.stop) {
 #ifdef PXS_STAMPS
     const unsigned long long w0 = stamp();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned long long w1 = stamp();
-    st.wait += w1 - w0;
 #endif
     const uint32_t type = hdr_type(m.x);
     const uint32_t len = 1u + (type == PAXISIM_MSG_P1B ? hdr_n(m.x) : 0u);
 #pragma unroll
-    for (uint32_t s = 0; s < NSMAX; s++) {
-      const bool hit = s == src;
-      pos[s] = opaque(pos[s]) + (hit ? len : 0u);
-      rem[s] = opaque(rem[s]) - (hit ? len : 0u);
-    }
+    for (uint32_t s = 0; s < NSMAX; s++) rem[s] = opaque(rem[s]) - (s == src ? len : 0u);
     total -= len;
+    if (len > 1u && jv > i + 1u) jv = i + 1u;          // later picks differ from the staged ones
 #ifdef PXS_STAMPS
     const unsigned long long q0 = stamp();
+    st.wait += q0 - w0;               // trip head: message decode and FIFO bookkeeping
 #endif
     uint32_t nsrc = 0, nri = 0;
     uint4 nm = make_uint4(0u, 0u, 0u, 0u);
     if (total) {
       pick(i + 1u, nsrc, nri);
-      nm = x.rec[nri];                                  // prefetch
+      if constexpr (STAGED) {
+        if (i + 1u < jv) nm = stage[(i + 1u) * LANES];  // staged
+        else nm = load_now(x.rec + nri);                // past the stage: a blocking load
+      } else {
+        nm = x.rec[nri];                                // no stage: one message ahead from HBM
+      }
     }
 #ifdef PXS_STAMPS
     const unsigned long long q1 = stamp();
@@ -417,7 +501,8 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
 #endif
     intent_flush<NT>(P, x);                             // one emit point for all lanes
 #ifdef PXS_STAMPS
-    st.flush += stamp() - q2;
+    fe = stamp();
+    st.flush += fe - q2;
 #endif
 #ifdef PXS_STAMPS
     st.trips += 1;
@@ -432,28 +517,63 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
     if (s < NS) x.l_cnt[((box0 + s) << 6) | x.lane] = 0;
   if (x.stop) atomicMin(&x.l_poison[x.lane], x.t);
 #ifdef PXS_STAMPS
-  st.loop += stamp() - s1;
+  {
+    const unsigned long long e = stamp();
+    st.loop += e - s1;
+    st.tail += e - fe;
+  }
 #endif
 }
 
 // ---------------------------------------------------------------------------
 // The step kernel: stage the LDS image, run S steps, write everything back.
 // ---------------------------------------------------------------------------
+// Waves per SIMD the register allocator must allow.  The dispatcher places a
+// workgroup of n waves only where every SIMD has ceil(n/4) free wave slots
+// (measured: tools/probe/vgpr_probe.hip), so a 5- or 9-wave workgroup of
+// cluster groups needs 3 slots per SIMD -> at most 168 VGPRs.
+#ifdef PXS_MIN_WAVES
+template <int NT> constexpr int min_waves() { return PXS_MIN_WAVES; }
+#else
+template <int NT> constexpr int min_waves() { return NT == 0 ? 4 : 3; }
+#endif
+
+// Instances that carry the LDS-staged merge loop.  Staging only pays where a
+// workgroup runs alone on its CU and has LDS to spare (9 replicas, ABD's 3/5);
+// elsewhere the second copy of the loop costs registers the packed cluster
+// groups need.  paxisim.hip mirrors this (stage_built_host) and sets J = 0.
+template <int NT, class Proto> constexpr bool stage_built() {
+  return Proto::kind == PAXISIM_ABD ? NT != 0 : NT == 9;
+}
+
+// The largest workgroup: as many N-wave cluster groups as min_waves slots per
+// SIMD hold.  One workgroup = P.G cluster groups of N waves; group g of
+// workgroup b is the 64-cluster tile b*G + g with its own LDS region of
+// P.lds_bytes.
+template <int NT> constexpr int max_threads() {
+  return NT == 0 ? 1024 : ((4 * min_waves<NT>()) / NT > 0 ? (4 * min_waves<NT>()) / NT : 1) * NT * 64;
+}
 template <int NT, class Proto>
-__global__ void __launch_bounds__(NT ? NT * 64 : 1024, 3) sim_steps(Params P, uint32_t t0, uint32_t nsteps) {
+__global__ void __launch_bounds__(max_threads<NT>(), min_waves<NT>()) sim_steps(Params P, uint32_t t0, uint32_t nsteps) {
   extern __shared__ uint4 lds[];
   const uint32_t N = nrep<NT>(P);
-  const uint32_t blk = blockIdx.x;
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint32_t grp = wave / N;
+  const uint32_t blk = blockIdx.x * P.G + grp;
   {
-    const uint4* g = reinterpret_cast<const uint4*>(P.image + (size_t)blk * P.img.bytes);
-    for (uint32_t k = threadIdx.x; k < P.img.bytes / 16u; k += blockDim.x) lds[k] = g[k];
+    const uint32_t nb = P.img.bytes / 16u;
+    const uint4* g = reinterpret_cast<const uint4*>(P.image + (size_t)blockIdx.x * P.G * P.img.bytes);
+    for (uint32_t k = threadIdx.x; k < P.G * nb; k += blockDim.x) {
+      const uint32_t gg = k / nb;
+      lds[gg * (P.lds_bytes / 16u) + (k - gg * nb)] = g[k];
+    }
   }
-  uint8_t* L = reinterpret_cast<uint8_t*>(lds);
+  uint8_t* L = reinterpret_cast<uint8_t*>(lds) + grp * P.lds_bytes;
   Rep<NT> x;
   x.lane = threadIdx.x & 63u;
-  // replica played by this wave, rotated per workgroup: the busiest replica
-  // (the leader) then sits on a different wave -> SIMD in neighbouring workgroups
-  x.r = (threadIdx.x >> 6) + blk % N;
+  // replica played by this wave, rotated per tile: the busiest replica (the
+  // leader) then sits on a different wave -> SIMD in neighbouring tiles
+  x.r = (wave - grp * N) + blk % N;
   if (x.r >= N) x.r -= N;
   x.blk = blk;
   x.c = (uint64_t)blk * LANES + x.lane;
@@ -471,30 +591,31 @@ __global__ void __launch_bounds__(NT ? NT * 64 : 1024, 3) sim_steps(Params P, ui
     const size_t i = rc(P, x.r, x.c);
     x.kc = P.kc[x.c];
     x.flags = P.flags[i];
-#pragma unroll
-    for (uint32_t d = 0; d < Rep<NT>::NL; d++) {
-      x.du[d] = d < N ? P.link_drop[krc(P, d, x.r, x.c)] : 0u;
-      x.su[d] = d < N ? P.link_slow[krc(P, d, x.r, x.c)] : 0u;
-    }
     Proto::template load<NT>(P, x);
   }
 #pragma unroll
-  for (uint32_t k = 0; k < PAXISIM_NMSG; k++) x.dv[k] = 0;
+  for (uint32_t k = 0; k < PAXISIM_NMSG / 2; k++) x.dvp[k] = 0;
   x.client = x.sent = x.dropped = x.discarded = x.commits = x.replies = 0;
   __syncthreads();
 
   uint32_t b0 = t0 % P.D;
 #ifdef PXS_STAMPS
-  Stamps st = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  Stamps st = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_begin;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_begin)::"memory");
 #endif
   for (uint32_t t = t0; t < t0 + nsteps; t++) {
     if (live && x.l_poison[x.lane] >= t) {
       x.t = t;
       x.b0 = b0;
 #ifdef PXS_STAMPS
-      replica_step<NT, Proto>(P, x, &st);
+      if (stage_built<NT, Proto>() && P.J) replica_step<NT, Proto, stage_built<NT, Proto>()>(P, x, &st);
+      else replica_step<NT, Proto, false>(P, x, &st);
 #else
-      replica_step<NT, Proto>(P, x);
+      if (stage_built<NT, Proto>() && P.J)
+        replica_step<NT, Proto, stage_built<NT, Proto>()>(P, x);   // records staged into LDS per step
+      else
+        replica_step<NT, Proto, false>(P, x);                     // one message ahead from HBM
 #endif
     }
     if (++b0 == P.D) b0 = 0;
@@ -514,28 +635,32 @@ __global__ void __launch_bounds__(NT ? NT * 64 : 1024, 3) sim_steps(Params P, ui
     atomicAdd(&d[3], st.trips); atomicAdd(&d[4], st.msgs); atomicAdd(&d[5], st.steps);
     atomicAdd(&d[6], st.pick); atomicAdd(&d[7], st.disp);
     atomicAdd(&d[8], st.wait); atomicAdd(&d[9], st.flush);
+    atomicAdd(&d[10], st.stage); atomicAdd(&d[11], st.tail);
+    unsigned long long t_end;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_end)::"memory");
+    d[12] = t_begin;                                        // residency: 100 MHz wall clock
+    d[13] = t_end;
+    d[14] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11));   // HW_ID
+    d[15] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((32 - 1) << 11));  // XCC_ID (gfx940+)
   }
 #endif
 
   {
-    uint4* g = reinterpret_cast<uint4*>(P.image + (size_t)blk * P.img.bytes);
-    for (uint32_t k = threadIdx.x; k < P.img.bytes / 16u; k += blockDim.x) g[k] = lds[k];
+    const uint32_t nb = P.img.bytes / 16u;
+    uint4* g = reinterpret_cast<uint4*>(P.image + (size_t)blockIdx.x * P.G * P.img.bytes);
+    for (uint32_t k = threadIdx.x; k < P.G * nb; k += blockDim.x) {
+      const uint32_t gg = k / nb;
+      g[k] = lds[gg * (P.lds_bytes / 16u) + (k - gg * nb)];
+    }
   }
   if (live) {
     const uint32_t r = x.r;
     const uint64_t c = x.c;
     P.flags[rc(P, r, c)] = x.flags;
-#pragma unroll
-    for (uint32_t d = 0; d < Rep<NT>::NL; d++) {
-      if (d < N) {
-        P.link_drop[krc(P, d, r, c)] = x.du[d];
-        P.link_slow[krc(P, d, r, c)] = x.su[d];
-      }
-    }
     Proto::template store<NT>(P, x);
 #pragma unroll
     for (uint32_t k = 1; k < PAXISIM_NMSG; k++)
-      if (x.dv[k]) P.stats[krc(P, ST_DELIV0 + k, r, c)] += x.dv[k];
+      if (dv_get(x, k)) P.stats[krc(P, ST_DELIV0 + k, r, c)] += dv_get(x, k);
     P.stats[krc(P, ST_CLIENT, r, c)] += x.client;
     P.stats[krc(P, ST_SENT, r, c)] += x.sent;
     P.stats[krc(P, ST_DROPPED, r, c)] += x.dropped;

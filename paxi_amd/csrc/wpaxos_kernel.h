@@ -115,6 +115,7 @@ __device__ __forceinline__ void wp_handle_request(const Params& P, Rep<NT>& x, u
 }
 
 struct WPaxosProto {
+  static constexpr uint32_t kind = PAXISIM_WPAXOS;
   template <int NT>
   __device__ static __forceinline__ void load(const Params& P, Rep<NT>& x) {
     x.nfwd = P.nfwd[rc(P, x.r, x.c)];
@@ -140,41 +141,41 @@ struct WPaxosProto {
                                                   uint32_t ri) {
     const uint32_t type = hdr_type(m.x);
     if (type == PAXISIM_MSG_REPLY) {                                   // node.recv (node.go:83-90)
-      x.dv[PAXISIM_MSG_REPLY]++;
+      dv_inc<NT>(x, PAXISIM_MSG_REPLY);
       handle_reply<NT>(P, x, m.w);
       return;
     }
     wp_bind<NT>(P, x, type == PAXISIM_MSG_REQUEST ? wl_key(P, x.kc, m.w) : hdr_key(m.x));
     switch (type) {
       case PAXISIM_MSG_REQUEST:
-        x.dv[PAXISIM_MSG_REQUEST]++;
+        dv_inc<NT>(x, PAXISIM_MSG_REQUEST);
         wp_handle_request<NT>(P, x, mkreq(m.w, src));
         break;
       case PAXISIM_MSG_P1A:                                            // handlePrepare 72-76
-        x.dv[PAXISIM_MSG_P1A]++;
+        dv_inc<NT>(x, PAXISIM_MSG_P1A);
         x.exists = 1;
         paxos_handle_p1a<NT>(P, x, m.y);
         break;
       case PAXISIM_MSG_P1B:                                            // handlePromise 78-82
-        x.dv[PAXISIM_MSG_P1B]++;
+        dv_inc<NT>(x, PAXISIM_MSG_P1B);
         if (wp_get<NT>(x)) paxos_handle_p1b<NT>(P, x, src, m.y, ri, hdr_n(m.x));
         break;
       case PAXISIM_MSG_P2A:                                            // handleAccept 84-88
-        x.dv[PAXISIM_MSG_P2A]++;
+        dv_inc<NT>(x, PAXISIM_MSG_P2A);
         x.exists = 1;
         paxos_handle_p2a<NT>(P, x, m.y, (int32_t)m.z, m.w);
         break;
       case PAXISIM_MSG_P2B:                                            // handleAccepted 90-93
-        x.dv[PAXISIM_MSG_P2B]++;
+        dv_inc<NT>(x, PAXISIM_MSG_P2B);
         if (wp_get<NT>(x)) paxos_handle_p2b<NT>(P, x, src, m.y, (int32_t)m.z);
         break;
       case PAXISIM_MSG_P3:                                             // handleCommit 95-99
-        x.dv[PAXISIM_MSG_P3]++;
+        dv_inc<NT>(x, PAXISIM_MSG_P3);
         x.exists = 1;
         paxos_handle_p3<NT>(P, x, m.y, (int32_t)m.z, m.w);
         break;
       case PAXISIM_MSG_LEADERCHG:                                      // handleLeaderChange 101-108
-        x.dv[PAXISIM_MSG_LEADERCHG]++;
+        dv_inc<NT>(x, PAXISIM_MSG_LEADERCHG);
         if (wp_get<NT>(x) && m.y == x.ballot && m.z == x.r) paxos_p1a<NT>(P, x);
         break;
       default: break;

@@ -13,7 +13,8 @@ import os
 from . import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpaxisim.so")
+# PAXISIM_LIB selects another build of the same HIP library (tuning variants)
+LIB_PATH = os.environ.get("PAXISIM_LIB") or os.path.join(_HERE, "libpaxisim.so")
 _lib = None
 
 
@@ -43,6 +44,8 @@ def load_library():
     L.paxisim_history.restype = C.c_int
     L.paxisim_history.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32), C.c_uint32,
                                   C.POINTER(C.c_uint32)]
+    L.paxisim_occupancy.restype = C.c_int
+    L.paxisim_occupancy.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     L.paxisim_device_bytes.restype = C.c_int
     L.paxisim_device_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     if L.paxisim_abi_version() != abi.ABI_VERSION:
@@ -54,7 +57,7 @@ def load_library():
 EXPORTED = ["paxisim_abi_version", "paxisim_last_error", "paxisim_create", "paxisim_destroy",
             "paxisim_fault_add", "paxisim_step", "paxisim_sync", "paxisim_stats_get",
             "paxisim_read_state", "paxisim_read_instances", "paxisim_check", "paxisim_kernel_time", "paxisim_device_bytes",
-            "paxisim_linearizable", "paxisim_history"]
+            "paxisim_linearizable", "paxisim_history", "paxisim_occupancy"]
 
 
 def _check(rc):
@@ -124,6 +127,12 @@ class Simulation:
         ms, n = C.c_double(), C.c_uint64()
         _check(load_library().paxisim_kernel_time(self.h, C.byref(ms), C.byref(n), int(reset)))
         return ms.value, n.value
+
+    def occupancy(self):
+        """(workgroups resident per CU, dynamic LDS bytes per workgroup, messages staged per replica-step)"""
+        b, lds, j = C.c_int(), C.c_uint32(), C.c_uint32()
+        _check(load_library().paxisim_occupancy(self.h, C.byref(b), C.byref(lds), C.byref(j)))
+        return b.value, lds.value, j.value
 
     def device_bytes(self):
         b = C.c_uint64()
