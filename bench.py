@@ -89,6 +89,24 @@ def workload(cfg_id, clusters, base, device, args):
     raise SystemExit(f"unknown config {cfg_id}")
 
 
+def measured_traffic(args, kernel, mbox):
+    """HBM bytes per launch of this exact workload from the PMC passes of
+    tools/traffic.sh (committed as profiles/traffic_config<c>.json).  The
+    simulation is seeded, so a launch moves the same bytes in every run of the
+    same workload; counters cannot be read from inside this process."""
+    path = os.path.join(ROOT, "profiles", f"traffic_config{args.config}.json")
+    try:
+        t = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    same = (t.get("kernel") == kernel and t.get("clusters_per_gpu") == args.clusters
+            and t.get("sim_steps_per_step") == args.sim_steps and t.get("window") == args.window
+            and t.get("mbox_cap") == mbox and t.get("steps") == args.steps and t.get("warmup") == args.warmup)
+    if not same:
+        return None
+    return {"bytes_per_launch": t["bytes_per_launch"], "source": os.path.relpath(path, ROOT)}
+
+
 def cpu_baseline(args):
     """The C oracle (same delivery schedule) on a bounded sample of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -223,6 +241,10 @@ def main():
                          "kernel": f"sim_steps<{abi.n_replicas(cfg)},{proto}>",
                          "avg_launch_ms": avg_launch_ms, "alg_bytes_per_launch": alg_bytes(d) / max(1, launches)},
         }
+        tr = measured_traffic(args, out["roofline"]["kernel"], cfg.mbox_cap)
+        if tr is not None:
+            out["roofline"]["traffic"] = tr["bytes_per_launch"]
+            out["roofline"]["traffic_source"] = tr["source"]
         if lin is not None:
             out["linearizability"] = lin
         if not args.no_cpu_baseline and world == 1:
