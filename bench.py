@@ -169,9 +169,16 @@ def main():
     rank, world, local = pdist.env_rank()
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # PAXISIM_DIST_BACKEND=gloo rehearses the N>1 flow with several ranks on
+    # one GPU (RCCL refuses two ranks on one device); the default is RCCL.
+    backend = os.environ.get("PAXISIM_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     def barrier():
         if world > 1:
@@ -206,7 +213,8 @@ def main():
         lin = {"anomalies": a, "ops_checked": n, "partitions_skipped": skipped, "scan_s": time.perf_counter() - tl}
 
     tot, (dt_max, kms_max) = pdist.reduce_counters(
-        pdist.stats_counters(d, alg_bytes(d), violations, s1["flagged"]), [dt, kms], device="cuda")
+        pdist.stats_counters(d, alg_bytes(d), violations, s1["flagged"]), [dt, kms],
+        device="cuda" if backend == "nccl" else "cpu")
 
     if rank == 0:
         avg_launch_ms = kms / max(1, launches)

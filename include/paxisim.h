@@ -35,11 +35,12 @@
 extern "C" {
 #endif
 
-#define PAXISIM_ABI_VERSION 3
+#define PAXISIM_ABI_VERSION 4
 
 #define PAXISIM_MAX_N        16  /* replicas per cluster (ack masks are u16) */
 #define PAXISIM_MAX_ZONES    16
 #define PAXISIM_MAX_WORKERS  32  /* closed-loop client workers per cluster */
+#define PAXISIM_MAX_KEYS     64  /* keys per cluster (workload key space) */
 #define PAXISIM_MAX_FAULTS   64  /* scripted fault windows per handle */
 #define PAXISIM_MAX_WINDOW   64  /* log window slots per replica */
 #define PAXISIM_MAX_MBOX     64  /* records per (link, arrival-step) bucket */
@@ -136,12 +137,27 @@ typedef struct paxisim_config {
   uint64_t seed;
 } paxisim_config;
 
+/* Key distributions of the benchmark's key generator (benchmark.go:202-244,
+ * Bconfig.Distribution).  Keys live in [0, keys); the key of a command is a
+ * pure function of (cluster, cid), so both backends agree. */
+enum paxisim_distribution {
+  PAXISIM_DIST_UNIFORM  = 0,  /* "uniform": rand.Intn(K) (benchmark.go:210-211)         */
+  PAXISIM_DIST_ORDER    = 1,  /* "order": counter+1 mod K, counter = cid (205-207)      */
+  PAXISIM_DIST_CONFLICT = 2,  /* "conflict": key 0 w.p. conflicts %, else order (213-219) */
+  PAXISIM_DIST_TABLE    = 3   /* "normal"/"zipfan"/"exponential" (221-233): inverse CDF
+                                 over key_cdf, built by the caller (paxi_amd.workload) */
+};
+
 typedef struct paxisim_workload {
   uint32_t outstanding;       /* closed-loop workers per cluster (Bconfig.Concurrency) */
   uint32_t max_requests;      /* per worker; 0 = unlimited (Bconfig.N) */
   uint32_t write_ppm;         /* P(write) in parts per million (Bconfig.W) */
   uint32_t locality_ppm;      /* WPaxos: P(key from the worker's own zone) */
   uint32_t target[PAXISIM_MAX_WORKERS]; /* replica each worker sends to */
+  uint32_t distribution;      /* enum paxisim_distribution: Bconfig.Distribution */
+  uint32_t conflicts;         /* CONFLICT: percent of commands on key 0 (Bconfig.Conflicts) */
+  uint32_t key_cdf[PAXISIM_MAX_KEYS]; /* TABLE: key = #{k < keys-1 : u32 draw >= key_cdf[k]};
+                                 non-decreasing over [0, keys-1) */
 } paxisim_workload;
 
 /* Random fault process, applied per (cluster, src, dst) link every step. */

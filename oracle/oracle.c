@@ -725,7 +725,21 @@ static inline uint32_t wl_key(const struct oracle_sim* s, uint32_t kc, uint32_t 
     const uint32_t nk = z < K ? (K - z + Z - 1u) / Z : 0u;
     if (nk && ppm_hit(fmix32(h ^ 0x165667B1u), s->wl.locality_ppm)) return z + Z * (h % nk);
   }
-  return h % K;
+  /* Bconfig.Distribution (benchmark.go:202-233) as a function of cid:
+   * "order" counter+1 mod K with the counter = cid (205-207); "conflict" key 0
+   * with rand.Intn(100) < Conflicts, else order (213-219); "normal", "zipfan",
+   * "exponential" (221-233) by inverse CDF over the caller's key_cdf table. */
+  switch (s->wl.distribution) {
+    case PAXISIM_DIST_ORDER: return cid % K;
+    case PAXISIM_DIST_CONFLICT: return fmix32(h ^ 0x3C6EF372u) % 100u < s->wl.conflicts ? 0u : cid % K;
+    case PAXISIM_DIST_TABLE: {
+      const uint32_t u = fmix32(h ^ 0x2545F491u);
+      uint32_t k = 0, i;
+      for (i = 0; i + 1u < K; i++) k += u >= s->wl.key_cdf[i] ? 1u : 0u;
+      return k;
+    }
+    default: return h % K;
+  }
 }
 static inline int wl_write(const struct oracle_sim* s, uint32_t kc, uint32_t cid) {
   return ppm_hit(fmix32(wl_hash(kc, cid) ^ 0x27D4EB2Fu), s->wl.write_ppm);
@@ -1037,6 +1051,11 @@ static int check_config(const paxisim_config* cfg, const paxisim_workload* wl,
   if (cfg->clusters < 1) return fail(PAXISIM_EINVAL, "clusters");
   if (wl->outstanding < 1 || wl->outstanding > PAXISIM_MAX_WORKERS) return fail(PAXISIM_EINVAL, "outstanding");
   if (wl->outstanding > cfg->mbox_cap) return fail(PAXISIM_EINVAL, "outstanding exceeds mbox_cap");
+  if (wl->distribution > PAXISIM_DIST_TABLE) return fail(PAXISIM_EINVAL, "distribution %u", wl->distribution);
+  if (wl->distribution == PAXISIM_DIST_CONFLICT && wl->conflicts > 100) return fail(PAXISIM_EINVAL, "conflicts > 100");
+  if (wl->distribution == PAXISIM_DIST_TABLE)
+    for (w = 1; w + 1u < cfg->keys; w++)
+      if (wl->key_cdf[w] < wl->key_cdf[w - 1]) return fail(PAXISIM_EINVAL, "key_cdf must be non-decreasing");
   for (w = 0; w < wl->outstanding; w++)
     if (wl->target[w] >= N) return fail(PAXISIM_EINVAL, "target[%u]", w);
   if (fp->slow_ppm && (fp->slow_min > fp->slow_max || fp->slow_max > cfg->max_delay))

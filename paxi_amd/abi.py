@@ -6,10 +6,11 @@ structs, so the two speak exactly the same ABI.
 """
 import ctypes as C
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_N = 16
 MAX_ZONES = 16
 MAX_WORKERS = 32
+MAX_KEYS = 64
 MAX_FAULTS = 64
 MAX_WINDOW = 64
 MAX_MBOX = 64
@@ -38,6 +39,9 @@ MSG_NAMES = {MSG_REQUEST: "Request", MSG_REPLY: "Reply", MSG_P1A: "P1a", MSG_P1B
 # flags
 F_WOVF, F_GHOST, F_MBOX_OVF, F_PEND_OVF, F_UNFAITHFUL, F_POISON, F_BALLOT_OVF, F_HIST_OVF = (
     0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80)
+
+# workload key distributions (benchmark.go:202-233)
+DIST_UNIFORM, DIST_ORDER, DIST_CONFLICT, DIST_TABLE = 0, 1, 2, 3
 
 # scripted faults (socket.go:163-199)
 FAULT_DROP, FAULT_SLOW, FAULT_FLAKY, FAULT_CRASH = 0, 1, 2, 3
@@ -75,6 +79,9 @@ class Workload(C.Structure):
         ("write_ppm", C.c_uint32),
         ("locality_ppm", C.c_uint32),
         ("target", C.c_uint32 * MAX_WORKERS),
+        ("distribution", C.c_uint32),
+        ("conflicts", C.c_uint32),
+        ("key_cdf", C.c_uint32 * MAX_KEYS),
     ]
 
 
@@ -188,11 +195,17 @@ def make_config(npz=(5,), protocol=PAXOS, q1=Q_MAJORITY, q2=Q_MAJORITY, fz=0, th
     return c
 
 
-def make_workload(outstanding=1, max_requests=0, write_ppm=1_000_000, locality_ppm=0, target=0):
+def make_workload(outstanding=1, max_requests=0, write_ppm=1_000_000, locality_ppm=0, target=0,
+                  distribution="uniform", keys=None, **dist_params):
+    """Closed-loop workload.  `distribution` is a Bconfig.Distribution name
+    (benchmark.go:202-233, see paxi_amd.workload); the table distributions
+    ("normal", "zipfan", "exponential") need the cluster's `keys`."""
+    from . import workload as _wl
     w = Workload()
     w.outstanding, w.max_requests, w.write_ppm, w.locality_ppm = outstanding, max_requests, write_ppm, locality_ppm
     for i in range(MAX_WORKERS):
         w.target[i] = target[i % len(target)] if isinstance(target, (list, tuple)) else target
+    _wl.set_distribution(w, distribution, keys, **dist_params)
     return w
 
 

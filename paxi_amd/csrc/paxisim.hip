@@ -310,6 +310,11 @@ static int check_config(const paxisim_config* cfg, const paxisim_workload* wl, c
   if (cfg->clusters < 1) return fail(PAXISIM_EINVAL, "clusters");
   if (wl->outstanding < 1 || wl->outstanding > PAXISIM_MAX_WORKERS) return fail(PAXISIM_EINVAL, "outstanding");
   if (wl->outstanding > cfg->mbox_cap) return fail(PAXISIM_EINVAL, "outstanding exceeds mbox_cap");
+  if (wl->distribution > PAXISIM_DIST_TABLE) return fail(PAXISIM_EINVAL, "distribution %u", wl->distribution);
+  if (wl->distribution == PAXISIM_DIST_CONFLICT && wl->conflicts > 100) return fail(PAXISIM_EINVAL, "conflicts > 100");
+  if (wl->distribution == PAXISIM_DIST_TABLE)
+    for (uint32_t k = 1; k + 1u < cfg->keys; k++)
+      if (wl->key_cdf[k] < wl->key_cdf[k - 1]) return fail(PAXISIM_EINVAL, "key_cdf must be non-decreasing");
   for (uint32_t w = 0; w < wl->outstanding; w++)
     if (wl->target[w] >= N) return fail(PAXISIM_EINVAL, "target[%u]", w);
   if (fp->slow_ppm && (fp->slow_min > fp->slow_max || fp->slow_max > cfg->max_delay))
@@ -394,6 +399,9 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
   P.keys = cfg->keys ? cfg->keys : 1;
   P.write_ppm = wl->write_ppm;
   P.locality_ppm = wl->locality_ppm;
+  P.dist = wl->distribution;
+  P.conflicts = wl->conflicts;
+  memcpy(P.key_cdf, wl->key_cdf, sizeof P.key_cdf);
   P.NK = cfg->protocol == PAXISIM_WPAXOS ? P.keys : 1u;
   P.NI = P.NK * N;
   P.adaptive = cfg->adaptive;

@@ -78,6 +78,8 @@ enum { ABD_FREE = 0, ABD_GET = 1, ABD_SET = 2, ABD_DONE = 3 };
 struct Params {
   uint32_t protocol, N, Z, W, M, D, NS, WK, max_requests;
   uint32_t keys, write_ppm, locality_ppm, H, OW;
+  uint32_t dist, conflicts;             // workload key distribution (paxisim_distribution)
+  uint32_t key_cdf[PAXISIM_MAX_KEYS];   // TABLE inverse CDF
   uint32_t NK, NI;       // Paxos instances per replica (WPaxos: keys, else 1); per cluster NI = NK*N
   uint32_t adaptive, policy_thr;
   uint32_t wk_magic;     // floor((2^32-1)/WK): (x % WK) by multiply-high + one correction

@@ -243,7 +243,18 @@ __device__ __forceinline__ uint32_t wl_key(const Params& P, uint32_t kc, uint32_
     const uint32_t nk = z < P.keys ? (P.keys - z + P.Z - 1u) / P.Z : 0u;
     if (nk && ppm_hit(fmix32(h ^ 0x165667B1u), P.locality_ppm)) return z + P.Z * (h % nk);
   }
-  return h % P.keys;
+  switch (P.dist) {   // Bconfig.Distribution (benchmark.go:202-233), DESIGN.md §3.8
+    case PAXISIM_DIST_ORDER: return cid % P.keys;
+    case PAXISIM_DIST_CONFLICT:
+      return fmix32(h ^ 0x3C6EF372u) % 100u < P.conflicts ? 0u : cid % P.keys;
+    case PAXISIM_DIST_TABLE: {   // inverse CDF; the table index is uniform, so these are scalar loads
+      const uint32_t u = fmix32(h ^ 0x2545F491u);
+      uint32_t k = 0;
+      for (uint32_t i = 0; i + 1u < P.keys; i++) k += u >= P.key_cdf[i] ? 1u : 0u;
+      return k;
+    }
+    default: return h % P.keys;
+  }
 }
 __device__ __forceinline__ bool wl_write(const Params& P, uint32_t kc, uint32_t cid) {
   return ppm_hit(fmix32(wl_hash(kc, cid) ^ 0x27D4EB2Fu), P.write_ppm);

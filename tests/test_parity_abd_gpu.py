@@ -10,10 +10,10 @@ pytestmark = pytest.mark.gpu
 
 
 def make(clusters, npz=(5,), outstanding=4, target=(0, 1, 2, 3), write_ppm=500_000, keys=8, history=64, seed=13,
-         fp=None, faults=()):
+         fp=None, faults=(), **dist):
     from paxi_amd.sim import Simulation
     cfg = abi.make_config(protocol=abi.ABD, npz=list(npz), clusters=clusters, seed=seed, keys=keys, history=history)
-    wl = abi.make_workload(outstanding=outstanding, target=list(target), write_ppm=write_ppm)
+    wl = abi.make_workload(outstanding=outstanding, target=list(target), write_ppm=write_ppm, keys=keys, **dist)
     return Simulation(cfg, wl, fp, faults), ol.OracleSim(cfg, wl, fp, faults)
 
 
@@ -52,3 +52,33 @@ def test_abd_with_faults(npz):
               abi.make_fault(abi.FAULT_FLAKY, 0, param=200_000, step_from=0, step_to=120)]
     g, o = make(256, npz=npz, target=(0, 1, 2, 0), fp=fp, faults=faults)
     same(g, o, [70, 80])
+
+
+@pytest.mark.parametrize("dist", [dict(distribution="order"), dict(distribution="conflict", conflicts=40),
+                                  dict(distribution="zipfan"), dict(distribution="normal", mu=3.0, sigma=5.0),
+                                  dict(distribution="exponential", lam=0.3)])
+def test_abd_key_distributions(dist):
+    """Bconfig.Distribution (benchmark.go:202-233): the GPU's key draws, and so
+    every op, history and the linearizability scan, match the oracle."""
+    g, o = make(192, keys=13, **dist)
+    same(g, o, [90, 40])
+
+
+def test_history_export_from_device(tmp_path):
+    """paxi_amd.history over the device's records equals the oracle's, and
+    WriteFile output (history.go:74-113) is byte-identical."""
+    from paxi_amd.history import History
+    g, o = make(16, keys=4, history=128)
+    same(g, o, [400])
+
+    class _O:
+        cfg = g.cfg
+
+        def history(self, c):
+            return o.history(c)
+    hg, ho = History.from_simulation(g), History.from_simulation(_O())
+    for c, (a, b) in enumerate(zip(hg, ho)):
+        a.write_file(str(tmp_path / f"g{c}"))
+        b.write_file(str(tmp_path / f"o{c}"))
+        assert (tmp_path / f"g{c}.csv").read_text() == (tmp_path / f"o{c}.csv").read_text()
+        assert len(a.operations) > 10

@@ -90,3 +90,14 @@ def test_reference_gap_reproduced_on_gpu():
     g.step(10)
     assert g.check() == 1
     g.close()
+
+
+@pytest.mark.parametrize("dist", [dict(distribution="zipfan"), dict(distribution="order"),
+                                  dict(distribution="conflict", conflicts=25)])
+def test_key_distributions(dist):
+    """WPaxos with the benchmark's key distributions (benchmark.go:202-233),
+    with and without zone locality."""
+    cfg = wp_config(160, keys=7)
+    for loc in (0, 500_000):
+        wl = abi.make_workload(outstanding=6, target=[0, 3, 6, 1, 4, 7], locality_ppm=loc, keys=7, **dist)
+        run_and_compare(cfg, wl, chunks=(120, 80))
