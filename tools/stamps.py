@@ -35,8 +35,8 @@ for r in range(5):
             tot[k] += buf[(b * 16 + r) * 16 + k]
     st = max(1, tot[5])
     print(f"replica {r}: per wave-step setup {tot[0]/st:8.0f} loop {tot[1]/st:8.0f} barrier {tot[2]/st:8.0f} cyc;"
-          f" trips {tot[3]/st:5.2f}, records/lane {tot[4]/st/64:5.2f};"
-          f" per trip: pick+prefetch {tot[6]/max(1,tot[3]):6.0f} dispatch {tot[7]/max(1,tot[3]):6.0f}"
+          f" lane-0 trips {tot[3]/st:5.2f}, records/lane {tot[4]/st/64:5.2f};"
+          f" per lane-0 trip: pick+prefetch {tot[6]/max(1,tot[3]):6.0f} dispatch {tot[7]/max(1,tot[3]):6.0f}"
           f" head {tot[8]/max(1,tot[3]):6.0f} flush {tot[9]/max(1,tot[3]):6.0f}"
           f" rest {(tot[1]-tot[6]-tot[7]-tot[8]-tot[9]-tot[10]-tot[11])/max(1,tot[3]):6.0f};"
-          f" per step: stage {tot[10]/st:7.0f} loop exit {tot[11]/st:7.0f}")
+          f" per step: stage {tot[10]/st:7.0f} after lane 0 done (other lanes trips) {tot[11]/st:7.0f}")
