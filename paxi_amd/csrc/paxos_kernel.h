@@ -450,6 +450,19 @@ struct PaxosProto {
   __device__ static __forceinline__ void client_request(const Params& P, Rep<NT>& x, uint32_t cid) {
     handle_request<NT>(P, x, mkreq(cid, PAXISIM_CLIENT_SRC));
   }
+  // True when HandleP2b (paxos.go:270-310) would return without touching any
+  // state: no entry (executed: G7), m.Ballot < e.ballot, or already committed;
+  // outside the window only where no flag could be raised (paxos_handle_p2b).
+  template <int NT>
+  __device__ static __forceinline__ bool ignorable(const Params& P, const Rep<NT>& x, const uint4& m) {
+    if (hdr_type(m.x) != PAXISIM_MSG_P2B) return false;
+    const int32_t ms = (int32_t)m.z;
+    if (!in_window<NT>(P, x, ms))
+      return ms < x.execute ? !(x.iflags & PAXISIM_F_GHOST) : !(x.iflags & PAXISIM_F_WOVF);
+    const uint32_t i = eidx<NT>(P, x, ms);
+    const uint32_t c = x.l_b[i];
+    return !(c & EF_EXISTS) || m.y < x.l_a[i] || (c & EF_COMMIT);
+  }
   // node.handle dispatch (node.go:104-115; registrations paxos/replica.go:33-38)
   template <int NT>
   __device__ static __forceinline__ void dispatch(const Params& P, Rep<NT>& x, uint32_t src, const uint4& m,

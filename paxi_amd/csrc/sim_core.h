@@ -511,6 +511,23 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
     st.disp += q2 - q1;
 #endif
     intent_flush<NT>(P, x);                             // one emit point for all lanes
+    if constexpr (!STAGED && Proto::kind == PAXISIM_PAXOS) {
+      // A next message whose handler cannot change any state (a late P2b:
+      // paxos.go:270-279) is consumed in this same trip.  Order, counters and
+      // state are unchanged; the lane needs one trip fewer, which shortens the
+      // wave's step where it is longest (the leader's bursts of P2bs).
+      if (total && !x.stop && nsrc != N && Proto::template ignorable<NT>(P, x, nm)) {
+        dv_inc<NT>(x, hdr_type(nm.x));
+#pragma unroll
+        for (uint32_t s = 0; s < NSMAX; s++) rem[s] = opaque(rem[s]) - (s == nsrc ? 1u : 0u);
+        total -= 1u;
+        i++;
+        if (total) {
+          pick(i + 1u, nsrc, nri);
+          nm = x.rec[nri];
+        }
+      }
+    }
 #ifdef PXS_STAMPS
     fe = stamp();
     st.flush += fe - q2;
