@@ -450,18 +450,33 @@ struct PaxosProto {
   __device__ static __forceinline__ void client_request(const Params& P, Rep<NT>& x, uint32_t cid) {
     handle_request<NT>(P, x, mkreq(cid, PAXISIM_CLIENT_SRC));
   }
-  // True when HandleP2b (paxos.go:270-310) would return without touching any
-  // state: no entry (executed: G7), m.Ballot < e.ballot, or already committed;
-  // outside the window only where no flag could be raised (paxos_handle_p2b).
+  // HandleP2b (paxos.go:270-310) for a P2b that neither completes a quorum
+  // nor poisons: returns true after applying it exactly as paxos_handle_p2b
+  // would (ignored: no entry (G7), m.Ballot < e.ballot, committed, or outside
+  // the window where no flag can be raised; else adopt a higher ballot and
+  // record the ack).  Returns false, with no effect, for every other message.
   template <int NT>
-  __device__ static __forceinline__ bool ignorable(const Params& P, const Rep<NT>& x, const uint4& m) {
+  __device__ static __forceinline__ bool absorb(const Params& P, Rep<NT>& x, uint32_t src, const uint4& m) {
     if (hdr_type(m.x) != PAXISIM_MSG_P2B) return false;
     const int32_t ms = (int32_t)m.z;
+    const uint32_t mb = m.y;
     if (!in_window<NT>(P, x, ms))
       return ms < x.execute ? !(x.iflags & PAXISIM_F_GHOST) : !(x.iflags & PAXISIM_F_WOVF);
     const uint32_t i = eidx<NT>(P, x, ms);
     const uint32_t c = x.l_b[i];
-    return !(c & EF_EXISTS) || m.y < x.l_a[i] || (c & EF_COMMIT);
+    const uint32_t eb = x.l_a[i];
+    if (!(c & EF_EXISTS) || mb < eb || (c & EF_COMMIT)) return true;
+    if (bal_id(mb) == x.r && mb == eb) {
+      if (!(c & EF_QUORUM)) return false;                 // nil quorum: the full handler poisons
+      const uint32_t ack = x.l_c[i] | (1u << src);
+      if (quorum_ok(P, P.q2, ack)) return false;          // commit: the full handler
+      x.l_c[i] = ack;
+    }
+    if (mb > x.ballot) {
+      x.ballot = mb;
+      x.active = 0;
+    }
+    return true;
   }
   // node.handle dispatch (node.go:104-115; registrations paxos/replica.go:33-38)
   template <int NT>

@@ -512,11 +512,15 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
 #endif
     intent_flush<NT>(P, x);                             // one emit point for all lanes
     if constexpr (!STAGED && Proto::kind == PAXISIM_PAXOS) {
-      // A next message whose handler cannot change any state (a late P2b:
-      // paxos.go:270-279) is consumed in this same trip.  Order, counters and
-      // state are unchanged; the lane needs one trip fewer, which shortens the
+      // Next messages whose handling is short and send-free (a P2b that does
+      // not complete a quorum: paxos.go:270-297) are handled in this same
+      // trip, up to ABSORB of them.  Order, counters and state are exactly as
+      // with one trip each; the lane needs fewer trips, which shortens the
       // wave's step where it is longest (the leader's bursts of P2bs).
-      if (total && !x.stop && nsrc != N && Proto::template ignorable<NT>(P, x, nm)) {
+      constexpr int ABSORB = 3;
+#pragma unroll
+      for (int k = 0; k < ABSORB; k++) {
+        if (!(total && !x.stop && nsrc != N && Proto::template absorb<NT>(P, x, nsrc, nm))) break;
         dv_inc<NT>(x, hdr_type(nm.x));
 #pragma unroll
         for (uint32_t s = 0; s < NSMAX; s++) rem[s] = opaque(rem[s]) - (s == nsrc ? 1u : 0u);
