@@ -1,0 +1,21 @@
+"""Average duration of the bench's timed step-kernel launches from a rocprofv3
+kernel trace (the last <steps> dispatches of sim_steps), to set beside
+bench.py's HIP-event average (roofline.avg_launch_ms).  The --stats summary
+averages every dispatch, warm-up included, and warm-up launches are faster
+(earlier simulation state).
+usage: python tools/prof_timed.py <run_kernel_trace.csv> <steps> [bench.json]"""
+import csv
+import json
+import sys
+
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if "sim_steps" in r["Kernel_Name"]]
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+steps = int(sys.argv[2])
+d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
+out = {"kernel": rows[-1]["Kernel_Name"], "dispatches": len(d), "timed": steps,
+       "rocprof_avg_timed_ms": sum(d[-steps:]) / steps, "rocprof_avg_all_ms": sum(d) / len(d)}
+if len(sys.argv) > 3:
+    b = json.load(open(sys.argv[3]))
+    out["bench_hip_event_avg_ms"] = b["roofline"]["avg_launch_ms"]
+    out["ratio"] = out["rocprof_avg_timed_ms"] / out["bench_hip_event_avg_ms"]
+print(json.dumps(out, indent=1))
