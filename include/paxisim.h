@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PAXISIM_ABI_VERSION 4
+#define PAXISIM_ABI_VERSION 5
 
 #define PAXISIM_MAX_N        16  /* replicas per cluster (ack masks are u16) */
 #define PAXISIM_MAX_ZONES    16
@@ -112,6 +112,16 @@ enum paxisim_fault_kind {
 };
 #define PAXISIM_ALL_DST 0xFFu
 
+/* WPaxos leader-migration policies (policy.go:15-47 NewPolicy, one per kpaxos,
+ * wpaxos/kpaxos.go:33).  Wall-clock time is the virtual step. */
+enum paxisim_policy {
+  PAXISIM_POLICY_CONSECUTIVE = 0, /* "consecutive" n = policy_threshold; 0 = "null" (policy.go:49-69) */
+  PAXISIM_POLICY_MAJORITY    = 1, /* "majority": an id with >= sum/2 of the hits in an interval of
+                                     policy_interval steps (policy.go:71-101) */
+  PAXISIM_POLICY_EMA         = 2  /* "ema": exponential moving average of the zone, alpha =
+                                     policy_alpha, epsilon 0.1 (policy.go:103-130) */
+};
+
 typedef struct paxisim_config {
   uint32_t protocol;          /* enum paxisim_protocol */
   uint32_t n_zones;           /* Z (config.go:113) */
@@ -135,6 +145,9 @@ typedef struct paxisim_config {
   uint64_t clusters;          /* clusters held by this handle */
   uint64_t cluster_base;      /* global id of local cluster 0 (multi-GPU sharding) */
   uint64_t seed;
+  uint32_t policy;            /* enum paxisim_policy: config.Policy */
+  uint32_t policy_interval;   /* MAJORITY: config.Threshold seconds, in steps (>= 1) */
+  double   policy_alpha;      /* EMA: config.Threshold, in (0, 1] */
 } paxisim_config;
 
 /* Key distributions of the benchmark's key generator (benchmark.go:202-244,
@@ -212,6 +225,8 @@ typedef struct paxisim_instance_state {
   uint64_t digest;            /* hash chain of executed (slot, command) */
   uint32_t policy_last;       /* consecutive policy (policy.go:49-69): last id, 0xFF = "" */
   uint32_t policy_hits;
+  uint32_t policy_state[4];   /* MAJORITY: {sum, interval start step, hash of the per-id hits, 0};
+                                 EMA: {s (float64 bits) lo, hi, zone, 0}; else 0 */
 } paxisim_instance_state;
 
 /* Whole-handle totals (sum over clusters and replicas). */

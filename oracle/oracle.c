@@ -12,6 +12,7 @@
  */
 #include "oracle.h"
 
+#include <math.h>
 #include <pthread.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -170,6 +171,10 @@ typedef struct inst {
   uint32_t nx, capx;
   /* WPaxos: r.paxi[key] != nil, and the consecutive policy (policy.go:49-69) */
   uint32_t exists, pol_last, pol_hits;
+  /* majority (policy.go:71-101): hits per id, their sum, interval start step;
+   * ema (policy.go:103-130): s and zone */
+  uint32_t pol_n[PAXISIM_MAX_N], pol_sum, pol_time, pol_zone;
+  double pol_s;
   uint32_t iflags;                 /* WOVF / GHOST raised on this instance's log */
   /* Uncommitted ghost entries Go would hold below execute: slot range and ballot range */
   uint32_t glo, ghi, gmin, gmax;
@@ -758,6 +763,7 @@ static inline void wp_bind(ctx_t* x, uint32_t key) {
 }
 static inline void wp_init(ctx_t* x, uint32_t key) {       /* Replica.init replica.go:36-40 */
   wp_bind(x, key);
+  if (!x->p->exists) x->p->pol_time = x->t;                /* newKPaxos -> NewPolicy: time.Now() */
   x->p->exists = 1;
 }
 /* r.paxi[m.Key] without init: a nil *kpaxos, whose use panics in Go */
@@ -769,10 +775,58 @@ static inline int wp_get(ctx_t* x, uint32_t key) {
   return 0;
 }
 
+/* majority.Hit (policy.go:79-93) with the step as the clock: an id holding
+ * at least sum/2 of the hits once `policy_interval` steps have passed since the
+ * last reset.  Go ranges over a map (random order) and keeps the last id that
+ * qualifies; here ids are visited in index order, so the highest index wins. */
+static uint32_t majority_hit(ctx_t* x, uint32_t id) {
+  inst_t* p = x->p;
+  const struct oracle_sim* s = x->s;
+  uint32_t res = POL_NONE, i;
+  if (p->pol_n[id] < 0xFFFFu) p->pol_n[id]++;              /* counters saturate at 16 bits */
+  p->pol_sum++;
+  if (p->pol_sum > 1 && x->t - p->pol_time >= s->cfg.policy_interval) {
+    for (i = 0; i < s->N; i++)
+      if (p->pol_n[i] >= p->pol_sum / 2) res = i;
+    for (i = 0; i < s->N; i++) p->pol_n[i] = 0;            /* reset (policy.go:95-101) */
+    p->pol_sum = 0;
+    p->pol_time = x->t;
+  }
+  return res;
+}
+
+/* ema.Hit (policy.go:111-130): s = alpha*zone + (1-alpha)*s, each operation
+ * rounded separately (no fused multiply-add); a settled s (within epsilon
+ * 0.1 of an integer) naming a new zone z returns NewID(z, 1). */
+static uint32_t ema_hit(ctx_t* x, uint32_t id) {
+  inst_t* p = x->p;
+  const struct oracle_sim* s = x->s;
+  const double a = s->cfg.policy_alpha, zid = (double)s->zone_of[id];
+  volatile double t1, t2, t3;                              /* keep every product rounded */
+  int32_t z;
+  uint32_t r = 0, k;
+  if (p->pol_s == 0.0) {
+    p->pol_s = zid;
+    return POL_NONE;
+  }
+  t1 = a * zid;
+  t2 = 1.0 - a;
+  t3 = t2 * p->pol_s;
+  p->pol_s = t1 + t3;
+  if (fabs(p->pol_s - round(p->pol_s)) > 0.1) return POL_NONE;
+  z = (int32_t)round(p->pol_s);
+  if ((uint32_t)z == p->pol_zone) return POL_NONE;
+  p->pol_zone = (uint32_t)z;
+  for (k = 0; k + 1u < (uint32_t)z; k++) r += s->cfg.npz[k]; /* index of ID z.1 */
+  return r;
+}
+
 /* consecutive.Hit (policy.go:55-69); threshold 0 is the null policy (policy.go:18-21) */
 static uint32_t policy_hit(ctx_t* x, uint32_t id) {
   inst_t* p = x->p;
   uint32_t res = POL_NONE;
+  if (x->s->cfg.policy == PAXISIM_POLICY_MAJORITY) return majority_hit(x, id);
+  if (x->s->cfg.policy == PAXISIM_POLICY_EMA) return ema_hit(x, id);
   if (x->s->cfg.policy_threshold == 0) return POL_NONE;
   if (id == p->pol_last) {
     p->pol_hits++;
@@ -1036,6 +1090,10 @@ static int check_config(const paxisim_config* cfg, const paxisim_workload* wl,
   if (cfg->protocol == PAXISIM_WPAXOS && (cfg->keys < 1 || cfg->keys > WP_KMAX))
     return fail(PAXISIM_EINVAL, "WPaxos keys must be in [1,%u]", WP_KMAX);
   if (cfg->policy_threshold > 255) return fail(PAXISIM_EINVAL, "policy_threshold");
+  if (cfg->policy > PAXISIM_POLICY_EMA) return fail(PAXISIM_EINVAL, "policy %u", cfg->policy);
+  if (cfg->policy == PAXISIM_POLICY_MAJORITY && cfg->policy_interval < 1) return fail(PAXISIM_EINVAL, "policy_interval");
+  if (cfg->policy == PAXISIM_POLICY_EMA && !(cfg->policy_alpha > 0.0 && cfg->policy_alpha <= 1.0))
+    return fail(PAXISIM_EINVAL, "policy_alpha must be in (0, 1]");
   if (wl->locality_ppm && cfg->keys < 1) return fail(PAXISIM_EINVAL, "locality needs keys");
   if (cfg->n_zones < 1 || cfg->n_zones > PAXISIM_MAX_ZONES) return fail(PAXISIM_EINVAL, "n_zones");
   for (z = 0; z < cfg->n_zones; z++) {
@@ -1326,6 +1384,19 @@ int oracle_read_instances(oracle_sim* s, uint64_t lo, uint64_t n, paxisim_instan
         o->digest = q->digest;
         o->policy_last = q->pol_last;
         o->policy_hits = q->pol_hits;
+        if (s->cfg.policy == PAXISIM_POLICY_MAJORITY) {
+          uint32_t h = 0x811C9DC5u, j;
+          for (j = 0; j < s->N; j++) h = fmix32(h ^ (q->pol_n[j] | j << 16));
+          o->policy_state[0] = q->pol_sum;
+          o->policy_state[1] = q->pol_time;
+          o->policy_state[2] = h;
+        } else if (s->cfg.policy == PAXISIM_POLICY_EMA) {
+          uint64_t b;
+          memcpy(&b, &q->pol_s, sizeof b);
+          o->policy_state[0] = (uint32_t)b;
+          o->policy_state[1] = (uint32_t)(b >> 32);
+          o->policy_state[2] = q->pol_zone;
+        }
       }
   return 0;
 }

@@ -6,7 +6,7 @@ structs, so the two speak exactly the same ABI.
 """
 import ctypes as C
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_N = 16
 MAX_ZONES = 16
 MAX_WORKERS = 32
@@ -40,6 +40,9 @@ MSG_NAMES = {MSG_REQUEST: "Request", MSG_REPLY: "Reply", MSG_P1A: "P1a", MSG_P1B
 F_WOVF, F_GHOST, F_MBOX_OVF, F_PEND_OVF, F_UNFAITHFUL, F_POISON, F_BALLOT_OVF, F_HIST_OVF = (
     0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80)
 
+# WPaxos leader-migration policies (policy.go)
+POLICY_CONSECUTIVE, POLICY_MAJORITY, POLICY_EMA = 0, 1, 2
+
 # workload key distributions (benchmark.go:202-233)
 DIST_UNIFORM, DIST_ORDER, DIST_CONFLICT, DIST_TABLE = 0, 1, 2, 3
 
@@ -69,6 +72,9 @@ class Config(C.Structure):
         ("clusters", C.c_uint64),
         ("cluster_base", C.c_uint64),
         ("seed", C.c_uint64),
+        ("policy", C.c_uint32),
+        ("policy_interval", C.c_uint32),
+        ("policy_alpha", C.c_double),
     ]
 
 
@@ -130,11 +136,12 @@ class InstanceState(C.Structure):
         ("p1_acks", C.c_uint32), ("npending", C.c_uint32),
         ("digest", C.c_uint64),
         ("policy_last", C.c_uint32), ("policy_hits", C.c_uint32),
+        ("policy_state", C.c_uint32 * 4),
     ]
 
     def as_tuple(self):
         return (self.ballot, self.slot, self.execute, self.active, self.exists, self.p1_acks,
-                self.npending, self.digest, self.policy_last, self.policy_hits)
+                self.npending, self.digest, self.policy_last, self.policy_hits, tuple(self.policy_state))
 
 
 class Stats(C.Structure):
@@ -180,7 +187,8 @@ def declare(lib, prefix):
 def make_config(npz=(5,), protocol=PAXOS, q1=Q_MAJORITY, q2=Q_MAJORITY, fz=0, thrifty=0,
                 ephemeral_leader=0, reply_when_commit=0, adaptive=1, policy_threshold=3,
                 window=16, mbox_cap=16, max_delay=4, keys=16, steps_per_launch=0, device=0,
-                clusters=1, cluster_base=0, seed=1, history=0):
+                clusters=1, cluster_base=0, seed=1, history=0, policy=POLICY_CONSECUTIVE, policy_interval=1,
+                policy_alpha=0.5):
     c = Config()
     c.protocol = protocol
     c.n_zones = len(npz)
@@ -192,6 +200,7 @@ def make_config(npz=(5,), protocol=PAXOS, q1=Q_MAJORITY, q2=Q_MAJORITY, fz=0, th
     c.window, c.mbox_cap, c.max_delay, c.keys = window, mbox_cap, max_delay, keys
     c.steps_per_launch, c.device, c.history = steps_per_launch, device, history
     c.clusters, c.cluster_base, c.seed = clusters, cluster_base, seed
+    c.policy, c.policy_interval, c.policy_alpha = policy, policy_interval, policy_alpha
     return c
 
 

@@ -219,6 +219,20 @@ __global__ void gather_inst_kernel(Params P, uint64_t lo, uint64_t n, paxisim_in
     s.digest = (uint64_t)b.y | ((uint64_t)b.z << 32);
     s.policy_last = b.w & 0xFFu;
     s.policy_hits = b.w >> 8;
+    if (P.policy == PAXISIM_POLICY_MAJORITY) {
+      const uint4 h0 = P.wpx[3 * si], h1 = P.wpx[3 * si + 1], m = P.wpx[3 * si + 2];
+      const uint32_t w[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+      uint32_t h = 0x811C9DC5u;
+      for (uint32_t j = 0; j < P.N; j++) h = fmix32(h ^ (((w[j >> 1] >> ((j & 1u) * 16u)) & 0xFFFFu) | j << 16));
+      s.policy_state[0] = m.x;
+      s.policy_state[1] = m.y;
+      s.policy_state[2] = h;
+    } else if (P.policy == PAXISIM_POLICY_EMA) {
+      const uint4 m = P.wpx[3 * si + 2];
+      s.policy_state[0] = m.x;
+      s.policy_state[1] = m.y;
+      s.policy_state[2] = m.z;
+    }
   } else {
     const size_t j = rc(P, r, c);
     s.ballot = P.ballot[j];
@@ -295,6 +309,10 @@ static int check_config(const paxisim_config* cfg, const paxisim_workload* wl, c
   if (cfg->protocol == PAXISIM_WPAXOS && (cfg->keys < 1 || cfg->keys > 32))
     return fail(PAXISIM_EINVAL, "WPaxos keys must be in [1,32]");
   if (cfg->policy_threshold > 255) return fail(PAXISIM_EINVAL, "policy_threshold");
+  if (cfg->policy > PAXISIM_POLICY_EMA) return fail(PAXISIM_EINVAL, "policy %u", cfg->policy);
+  if (cfg->policy == PAXISIM_POLICY_MAJORITY && cfg->policy_interval < 1) return fail(PAXISIM_EINVAL, "policy_interval");
+  if (cfg->policy == PAXISIM_POLICY_EMA && !(cfg->policy_alpha > 0.0 && cfg->policy_alpha <= 1.0))
+    return fail(PAXISIM_EINVAL, "policy_alpha must be in (0, 1]");
   if (cfg->n_zones < 1 || cfg->n_zones > PAXISIM_MAX_ZONES) return fail(PAXISIM_EINVAL, "n_zones");
   for (uint32_t z = 0; z < cfg->n_zones; z++) {
     if (cfg->npz[z] < 1) return fail(PAXISIM_EINVAL, "npz[%u] must be >= 1", z);
@@ -406,6 +424,9 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
   P.NI = P.NK * N;
   P.adaptive = cfg->adaptive;
   P.policy_thr = cfg->policy_threshold;
+  P.policy = cfg->policy;
+  P.policy_interval = cfg->policy_interval;
+  P.policy_alpha = cfg->policy_alpha;
   P.H = cfg->protocol == PAXISIM_ABD ? cfg->history : 0;
   P.OW = abd_ow(wl->outstanding);
   P.W = cfg->window;
@@ -496,6 +517,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     uint4* wst = carve<uint4>(p, wp ? NIC * 2 : 0);
     uint32_t* wlog = carve<uint32_t>(p, wp ? NIC * P.W * 4 : 0);
     uint32_t* wpend = carve<uint32_t>(p, wp ? NIC * PMAX : 0);
+    uint4* wpx = carve<uint4>(p, wp && cfg->policy != PAXISIM_POLICY_CONSECUTIVE ? NIC * 3 : 0);
     uint4* hist = carve<uint4>(p, NC * P.H);
     uint8_t* image = carve<uint8_t>(p, blocks * P.img.bytes);
     char* zend = p;
@@ -506,7 +528,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
       P.digest = dg; P.kc = kc; P.pend = pend; P.fwd = fwd;
       P.link_drop = links; P.link_slow = links + NC * N;
       P.ck_e = cke; P.ck_d = ckd; P.stats = st; P.reqx = reqx; P.hist = hist; P.image = image; P.rec = rec;
-      P.wst = wst; P.wlog = wlog; P.wpend = wpend; P.gst = gst;
+      P.wst = wst; P.wlog = wlog; P.wpend = wpend; P.gst = gst; P.wpx = wpx;
     }
     return std::make_pair((size_t)zend, (size_t)p);
   };

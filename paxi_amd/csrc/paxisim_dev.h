@@ -82,6 +82,8 @@ struct Params {
   uint32_t key_cdf[PAXISIM_MAX_KEYS];   // TABLE inverse CDF
   uint32_t NK, NI;       // Paxos instances per replica (WPaxos: keys, else 1); per cluster NI = NK*N
   uint32_t adaptive, policy_thr;
+  uint32_t policy, policy_interval;   // paxisim_policy; MAJORITY interval in steps
+  double policy_alpha;                // EMA alpha
   uint32_t wk_magic;     // floor((2^32-1)/WK): (x % WK) by multiply-high + one correction
   uint64_t C;            // allocated cluster lanes (multiple of 64)
   uint64_t clusters;     // live clusters
@@ -113,6 +115,7 @@ struct Params {
   uint4* wst;            // [blk][K][N][64][2]
   uint32_t* wlog;        // [blk][K][N][64][W][4]
   uint32_t* wpend;       // [blk][K][N][64][PMAX]
+  uint4* wpx;            // [blk][K][N][64][3] majority {hits u16 x 16 (2 x uint4), {sum, start step}} / ema {s lo, s hi, zone}
   uint32_t* stats;       // [NSTAT][N][C]
   uint32_t* reqx;        // [blk][N][W][64] request side table (Paxos)
   uint4* hist;           // [N][C][H] completed ABD ops {key|write<<31, value, start, end}

@@ -511,7 +511,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
     st.disp += q2 - q1;
 #endif
     intent_flush<NT>(P, x);                             // one emit point for all lanes
-    if constexpr (!STAGED && Proto::kind == PAXISIM_PAXOS) {
+    if constexpr (Proto::kind == PAXISIM_PAXOS) {
       // Next messages whose handling is short and send-free (a P2b that does
       // not complete a quorum: paxos.go:270-297) are handled in this same
       // trip, up to ABSORB of them.  Order, counters and state are exactly as
@@ -528,7 +528,8 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
         i++;
         if (total) {
           pick(i + 1u, nsrc, nri);
-          nm = x.rec[nri];
+          if constexpr (STAGED) nm = i + 1u < jv ? stage[(i + 1u) * LANES] : load_now(x.rec + nri);
+          else nm = x.rec[nri];
         }
       }
     }

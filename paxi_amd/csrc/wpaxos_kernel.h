@@ -74,9 +74,82 @@ __device__ __forceinline__ bool wp_get(Rep<NT>& x) {
   return false;
 }
 
+// Replica.init (replica.go:36-40): a new kpaxos gets a new policy, whose
+// majority interval starts now (policy.go:35, NewPolicy)
+template <int NT>
+__device__ __forceinline__ void wp_create(const Params& P, Rep<NT>& x) {
+  if (!x.exists && P.policy == PAXISIM_POLICY_MAJORITY)
+    P.wpx[3 * wp_slot<NT>(P, x, x.key) + 2] = make_uint4(0u, x.t, 0u, 0u);
+  x.exists = 1;
+}
+
+// majority.Hit (policy.go:79-93), the step as the clock; ids visited in index
+// order where Go ranges over a map, so the highest qualifying index wins
+template <int NT>
+__device__ __forceinline__ uint32_t majority_hit(const Params& P, Rep<NT>& x, uint32_t id) {
+  uint4* q = P.wpx + 3 * wp_slot<NT>(P, x, x.key);
+  const uint4 h0 = q[0], h1 = q[1];
+  uint4 m = q[2];
+  uint32_t w[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+  const uint32_t sh = (id & 1u) * 16u;
+#pragma unroll
+  for (uint32_t k = 0; k < 8; k++)
+    if (k == (id >> 1) && ((w[k] >> sh) & 0xFFFFu) < 0xFFFFu) w[k] += 1u << sh;   // saturating u16
+  m.x++;
+  uint32_t res = POL_NONE;
+  if (m.x > 1u && x.t - m.y >= P.policy_interval) {
+#pragma unroll
+    for (uint32_t i = 0; i < 16; i++)
+      if (i < nrep<NT>(P) && ((w[i >> 1] >> ((i & 1u) * 16u)) & 0xFFFFu) >= m.x / 2u) res = i;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) w[k] = 0;                                   // reset (policy.go:95-101)
+    m.x = 0;
+    m.y = x.t;
+  }
+  q[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  q[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  q[2] = m;
+  return res;
+}
+
+// ema.Hit (policy.go:111-130): every operation rounded on its own, as the
+// oracle computes it.  Measured: __dmul_rn/__dadd_rn alone still let the
+// compiler fuse the product into the sum (1-ulp parity failures), so the
+// products go through an asm barrier.
+template <int NT>
+__device__ __forceinline__ uint32_t ema_hit(const Params& P, Rep<NT>& x, uint32_t id) {
+  uint4* q = P.wpx + 3 * wp_slot<NT>(P, x, x.key);
+  uint4 m = q[2];
+  double s = __hiloint2double((int)m.y, (int)m.x);
+  const double zid = (double)(P.zone_of[id] + 1u);
+  uint32_t res = POL_NONE;
+  if (s == 0.0) {
+    s = zid;
+  } else {
+#pragma clang fp contract(off)
+    double t1 = P.policy_alpha * zid;
+    double t3 = (1.0 - P.policy_alpha) * s;
+    asm volatile("" : "+v"(t1), "+v"(t3));   // the products are rounded before the sum: no FMA
+    s = t1 + t3;
+    if (!(fabs(s - round(s)) > 0.1)) {
+      const uint32_t z = (uint32_t)(int32_t)round(s);
+      if (z != m.z) {
+        m.z = z;
+        res = __ffs(P.zmask[z - 1u]) - 1u;                                      // NewID(z, 1)
+      }
+    }
+  }
+  m.x = (uint32_t)__double2loint(s);
+  m.y = (uint32_t)__double2hiint(s);
+  q[2] = m;
+  return res;
+}
+
 // consecutive.Hit (policy.go:55-69); threshold 0 is the null policy (policy.go:18-21)
 template <int NT>
 __device__ __forceinline__ uint32_t policy_hit(const Params& P, Rep<NT>& x, uint32_t id) {
+  if (P.policy == PAXISIM_POLICY_MAJORITY) return majority_hit<NT>(P, x, id);
+  if (P.policy == PAXISIM_POLICY_EMA) return ema_hit<NT>(P, x, id);
   if (P.policy_thr == 0) return POL_NONE;
   uint32_t last = x.pol & 0xFFu, hits = x.pol >> 8;
   if (id == last) {
@@ -97,7 +170,7 @@ __device__ __forceinline__ uint32_t policy_hit(const Params& P, Rep<NT>& x, uint
 
 template <int NT>
 __device__ __forceinline__ void wp_handle_request(const Params& P, Rep<NT>& x, uint32_t req) {  // replica.go:42-66
-  x.exists = 1;                                                        // r.init(key)
+  wp_create<NT>(P, x);                                                 // r.init(key)
   if (!P.adaptive) {
     paxos_handle_request<NT>(P, x, req);
     return;
@@ -153,7 +226,7 @@ struct WPaxosProto {
         break;
       case PAXISIM_MSG_P1A:                                            // handlePrepare 72-76
         dv_inc<NT>(x, PAXISIM_MSG_P1A);
-        x.exists = 1;
+        wp_create<NT>(P, x);
         paxos_handle_p1a<NT>(P, x, m.y);
         break;
       case PAXISIM_MSG_P1B:                                            // handlePromise 78-82
@@ -162,7 +235,7 @@ struct WPaxosProto {
         break;
       case PAXISIM_MSG_P2A:                                            // handleAccept 84-88
         dv_inc<NT>(x, PAXISIM_MSG_P2A);
-        x.exists = 1;
+        wp_create<NT>(P, x);
         paxos_handle_p2a<NT>(P, x, m.y, (int32_t)m.z, m.w);
         break;
       case PAXISIM_MSG_P2B:                                            // handleAccepted 90-93
@@ -171,7 +244,7 @@ struct WPaxosProto {
         break;
       case PAXISIM_MSG_P3:                                             // handleCommit 95-99
         dv_inc<NT>(x, PAXISIM_MSG_P3);
-        x.exists = 1;
+        wp_create<NT>(P, x);
         paxos_handle_p3<NT>(P, x, m.y, (int32_t)m.z, m.w);
         break;
       case PAXISIM_MSG_LEADERCHG:                                      // handleLeaderChange 101-108

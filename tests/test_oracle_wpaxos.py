@@ -139,3 +139,54 @@ def test_key_range_rejected(keys):
     cfg = wp_config(clusters=1, keys=keys)
     with pytest.raises(RuntimeError):
         ol.OracleSim(cfg, abi.make_workload(outstanding=1))
+
+
+def _policy_run(policy, clusters=48, steps=1200, **kw):
+    cfg = wp_config(clusters=clusters, policy=policy, **kw)
+    wl = abi.make_workload(outstanding=9, target=list(range(9)), locality_ppm=700_000)
+    o = ol.OracleSim(cfg, wl)
+    o.step(steps)
+    return o, o.stats().as_dict(), o.read_instances()
+
+
+@pytest.mark.parametrize("interval", [1, 10, 60])
+def test_majority_policy_migrates_and_resets_per_interval(interval):
+    """majority.Hit (policy.go:79-101): LeaderChanges happen, and every instance's
+    interval started no later than now and is at most `interval` old unless idle."""
+    o, st, ins = _policy_run(abi.POLICY_MAJORITY, policy_interval=interval)
+    assert st["commits"] > 0 and st["flagged"][5] == 0
+    assert st["delivered"]["LeaderChange"] > 0
+    for s in ins:
+        if s.exists:
+            assert s.policy_state[1] <= 1200
+    # shorter intervals decide more often
+    if interval == 1:
+        _, st60, _ = _policy_run(abi.POLICY_MAJORITY, policy_interval=60)
+        assert st["delivered"]["LeaderChange"] > st60["delivered"]["LeaderChange"]
+
+
+@pytest.mark.parametrize("alpha", [0.3, 0.7, 1.0])
+def test_ema_policy_state(alpha):
+    """ema.Hit (policy.go:111-130): s stays within [1, Z] and the settled zone is
+    one of the zones; alpha = 1 follows the last requester's zone."""
+    import struct
+    o, st, ins = _policy_run(abi.POLICY_EMA, policy_alpha=alpha)
+    assert st["commits"] > 0 and st["flagged"][5] == 0
+    seen = 0
+    for s in ins:
+        if not s.exists:
+            continue
+        v = struct.unpack("<d", struct.pack("<II", s.policy_state[0], s.policy_state[1]))[0]
+        assert v == 0.0 or 1.0 <= v <= Z
+        assert s.policy_state[2] <= Z
+        seen += v != 0.0
+    assert seen > 0
+    assert st["delivered"]["LeaderChange"] > 0
+
+
+def test_policy_config_is_validated():
+    wl = abi.make_workload(outstanding=9, target=list(range(9)))
+    for kw in (dict(policy=3), dict(policy=abi.POLICY_MAJORITY, policy_interval=0),
+               dict(policy=abi.POLICY_EMA, policy_alpha=0.0), dict(policy=abi.POLICY_EMA, policy_alpha=1.5)):
+        with pytest.raises(RuntimeError):
+            ol.OracleSim(wp_config(clusters=2, **kw), wl)

@@ -101,3 +101,17 @@ def test_key_distributions(dist):
     for loc in (0, 500_000):
         wl = abi.make_workload(outstanding=6, target=[0, 3, 6, 1, 4, 7], locality_ppm=loc, keys=7, **dist)
         run_and_compare(cfg, wl, chunks=(120, 80))
+
+
+@pytest.mark.parametrize("policy,kw", [(abi.POLICY_MAJORITY, dict(policy_interval=1)),
+                                       (abi.POLICY_MAJORITY, dict(policy_interval=25)),
+                                       (abi.POLICY_EMA, dict(policy_alpha=0.3)),
+                                       (abi.POLICY_EMA, dict(policy_alpha=0.85))])
+def test_majority_and_ema_policies(policy, kw):
+    """majority / ema leader migration (policy.go:71-130) with the step as the
+    clock: instance state incl. the policy state is bit-exact."""
+    cfg = wp_config(192, keys=6, policy=policy, **kw)
+    wl = abi.make_workload(outstanding=9, target=list(range(9)), locality_ppm=600_000)
+    fp = abi.make_fault_process(drop_ppm=2000, drop_len=20)
+    st = run_and_compare(cfg, wl, fp, chunks=(250, 150))
+    assert st["delivered"]["LeaderChange"] > 0
