@@ -152,6 +152,29 @@ struct AbdProto {
   __device__ static __forceinline__ void client_request(const Params& P, Rep<NT>& x, uint32_t cid) {
     abd_handle_request<NT>(P, x, cid);
   }
+  // A GetReply or SetReply that does not complete its majority sends nothing
+  // (replica.go:97-157): apply it as the full handler would and return true
+  // (a late reply to a retired op or a finished phase is ignored).  Returns
+  // false, with no effect, for every other message.
+  template <int NT>
+  __device__ static __forceinline__ bool absorb(const Params& P, Rep<NT>& x, uint32_t src, const uint4& m) {
+    const uint32_t type = hdr_type(m.x), opid = m.y;
+    if (type != PAXISIM_MSG_GETREPLY && type != PAXISIM_MSG_SETREPLY) return false;
+    if (x.l_c[op_i<NT>(P, x, opid, 0)] != opid) return true;
+    const uint32_t si = op_i<NT>(P, x, opid, 2);
+    const uint32_t sm = x.l_c[si];
+    if (type == PAXISIM_MSG_SETREPLY) {
+      if ((sm & 3u) != ABD_SET) return true;
+      const uint32_t s2 = sm | ((1u << src) << 17);
+      if (abd_majority<NT>(P, s2 >> 17)) return false;            // Done: the full handler
+      x.l_c[si] = s2;
+      return true;
+    }
+    if ((sm & 3u) != ABD_GET) return true;
+    if (abd_majority<NT>(P, ((sm | ((1u << src) << 2)) >> 2) & 0x7FFFu)) return false;   // Set phase
+    abd_handle_getreply<NT>(P, x, src, hdr_n(m.x), opid, m.z, m.w);
+    return true;
+  }
   // registrations abd/replica.go:42-46
   template <int NT>
   __device__ static __forceinline__ void dispatch(const Params& P, Rep<NT>& x, uint32_t src, const uint4& m,

@@ -323,6 +323,15 @@ __device__ __forceinline__ void fault_process(const Params& P, Rep<NT>& x, uint3
   }
 }
 
+// Same-trip absorption of send-free P2bs (below) in the 9-replica Paxos
+// kernel too; 0 builds it without (A/B of register pressure vs trips).
+#ifndef PXS_ABSORB9
+#define PXS_ABSORB9 1
+#endif
+#ifndef PXS_ABSORB_ABD
+#define PXS_ABSORB_ABD 0
+#endif
+
 // ---------------------------------------------------------------------------
 // One replica, one step
 // ---------------------------------------------------------------------------
@@ -511,7 +520,8 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
     st.disp += q2 - q1;
 #endif
     intent_flush<NT>(P, x);                             // one emit point for all lanes
-    if constexpr (Proto::kind == PAXISIM_PAXOS) {
+    if constexpr ((Proto::kind == PAXISIM_PAXOS && (PXS_ABSORB9 || NT != 9)) ||
+                  (Proto::kind == PAXISIM_ABD && PXS_ABSORB_ABD)) {
       // Next messages whose handling is short and send-free (a P2b that does
       // not complete a quorum: paxos.go:270-297) are handled in this same
       // trip, up to ABSORB of them.  Order, counters and state are exactly as
