@@ -328,6 +328,9 @@ __device__ __forceinline__ void fault_process(const Params& P, Rep<NT>& x, uint3
 #ifndef PXS_ABSORB9
 #define PXS_ABSORB9 1
 #endif
+#ifndef PXS_ABSORB_MAX
+#define PXS_ABSORB_MAX 3   // messages absorbed per trip
+#endif
 #ifndef PXS_ABSORB_ABD
 #define PXS_ABSORB_ABD 0
 #endif
@@ -524,12 +527,11 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
                   (Proto::kind == PAXISIM_ABD && PXS_ABSORB_ABD)) {
       // Next messages whose handling is short and send-free (a P2b that does
       // not complete a quorum: paxos.go:270-297) are handled in this same
-      // trip, up to ABSORB of them.  Order, counters and state are exactly as
+      // trip, up to PXS_ABSORB_MAX of them.  Order, counters and state are exactly as
       // with one trip each; the lane needs fewer trips, which shortens the
       // wave's step where it is longest (the leader's bursts of P2bs).
-      constexpr int ABSORB = 3;
 #pragma unroll
-      for (int k = 0; k < ABSORB; k++) {
+      for (int k = 0; k < PXS_ABSORB_MAX; k++) {
         if (!(total && !x.stop && nsrc != N && Proto::template absorb<NT>(P, x, nsrc, nm))) break;
         dv_inc<NT>(x, hdr_type(nm.x));
 #pragma unroll

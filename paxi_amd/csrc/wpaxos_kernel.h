@@ -27,6 +27,14 @@ namespace pxs {
 
 constexpr uint32_t POL_NONE = 0xFFu;   // consecutive.last == "" (policy.go:50)
 
+// The majority / ema policies run only on a leader's request path; built out
+// of line (PXS_POLICY_NOINLINE=1) they stay out of the merge loop's registers.
+#if defined(PXS_POLICY_NOINLINE) && PXS_POLICY_NOINLINE
+#define PXS_POLICY_FN __device__ __attribute__((noinline))
+#else
+#define PXS_POLICY_FN __device__ __forceinline__
+#endif
+
 template <int NT>
 __device__ __forceinline__ size_t wp_slot(const Params& P, const Rep<NT>& x, uint32_t key) {
   return (((size_t)x.blk * P.keys + key) * nrep<NT>(P) + x.r) * LANES + x.lane;
@@ -86,8 +94,7 @@ __device__ __forceinline__ void wp_create(const Params& P, Rep<NT>& x) {
 // majority.Hit (policy.go:79-93), the step as the clock; ids visited in index
 // order where Go ranges over a map, so the highest qualifying index wins
 template <int NT>
-__device__ __forceinline__ uint32_t majority_hit(const Params& P, Rep<NT>& x, uint32_t id) {
-  uint4* q = P.wpx + 3 * wp_slot<NT>(P, x, x.key);
+PXS_POLICY_FN uint32_t majority_hit(uint4* q, uint32_t t, uint32_t id, uint32_t n, uint32_t interval) {
   const uint4 h0 = q[0], h1 = q[1];
   uint4 m = q[2];
   uint32_t w[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
@@ -97,14 +104,14 @@ __device__ __forceinline__ uint32_t majority_hit(const Params& P, Rep<NT>& x, ui
     if (k == (id >> 1) && ((w[k] >> sh) & 0xFFFFu) < 0xFFFFu) w[k] += 1u << sh;   // saturating u16
   m.x++;
   uint32_t res = POL_NONE;
-  if (m.x > 1u && x.t - m.y >= P.policy_interval) {
+  if (m.x > 1u && t - m.y >= interval) {
 #pragma unroll
     for (uint32_t i = 0; i < 16; i++)
-      if (i < nrep<NT>(P) && ((w[i >> 1] >> ((i & 1u) * 16u)) & 0xFFFFu) >= m.x / 2u) res = i;
+      if (i < n && ((w[i >> 1] >> ((i & 1u) * 16u)) & 0xFFFFu) >= m.x / 2u) res = i;
 #pragma unroll
     for (uint32_t k = 0; k < 8; k++) w[k] = 0;                                   // reset (policy.go:95-101)
     m.x = 0;
-    m.y = x.t;
+    m.y = t;
   }
   q[0] = make_uint4(w[0], w[1], w[2], w[3]);
   q[1] = make_uint4(w[4], w[5], w[6], w[7]);
@@ -115,27 +122,26 @@ __device__ __forceinline__ uint32_t majority_hit(const Params& P, Rep<NT>& x, ui
 // ema.Hit (policy.go:111-130): every operation rounded on its own, as the
 // oracle computes it.  Measured: __dmul_rn/__dadd_rn alone still let the
 // compiler fuse the product into the sum (1-ulp parity failures), so the
-// products go through an asm barrier.
+// products go through an asm barrier.  Returns the new settled zone
+// (1-based), or 0.
 template <int NT>
-__device__ __forceinline__ uint32_t ema_hit(const Params& P, Rep<NT>& x, uint32_t id) {
-  uint4* q = P.wpx + 3 * wp_slot<NT>(P, x, x.key);
+PXS_POLICY_FN uint32_t ema_hit(uint4* q, double alpha, double zid) {
   uint4 m = q[2];
   double s = __hiloint2double((int)m.y, (int)m.x);
-  const double zid = (double)(P.zone_of[id] + 1u);
-  uint32_t res = POL_NONE;
+  uint32_t res = 0;
   if (s == 0.0) {
     s = zid;
   } else {
 #pragma clang fp contract(off)
-    double t1 = P.policy_alpha * zid;
-    double t3 = (1.0 - P.policy_alpha) * s;
+    double t1 = alpha * zid;
+    double t3 = (1.0 - alpha) * s;
     asm volatile("" : "+v"(t1), "+v"(t3));   // the products are rounded before the sum: no FMA
     s = t1 + t3;
     if (!(fabs(s - round(s)) > 0.1)) {
       const uint32_t z = (uint32_t)(int32_t)round(s);
       if (z != m.z) {
         m.z = z;
-        res = __ffs(P.zmask[z - 1u]) - 1u;                                      // NewID(z, 1)
+        res = z;
       }
     }
   }
@@ -148,8 +154,13 @@ __device__ __forceinline__ uint32_t ema_hit(const Params& P, Rep<NT>& x, uint32_
 // consecutive.Hit (policy.go:55-69); threshold 0 is the null policy (policy.go:18-21)
 template <int NT>
 __device__ __forceinline__ uint32_t policy_hit(const Params& P, Rep<NT>& x, uint32_t id) {
-  if (P.policy == PAXISIM_POLICY_MAJORITY) return majority_hit<NT>(P, x, id);
-  if (P.policy == PAXISIM_POLICY_EMA) return ema_hit<NT>(P, x, id);
+  if (P.policy == PAXISIM_POLICY_MAJORITY)
+    return majority_hit<NT>(P.wpx + 3 * wp_slot<NT>(P, x, x.key), x.t, id, nrep<NT>(P), P.policy_interval);
+  if (P.policy == PAXISIM_POLICY_EMA) {
+    const uint32_t z = ema_hit<NT>(P.wpx + 3 * wp_slot<NT>(P, x, x.key), P.policy_alpha,
+                                   (double)(P.zone_of[id] + 1u));
+    return z ? (uint32_t)__ffs(P.zmask[z - 1u]) - 1u : POL_NONE;                 // NewID(z, 1)
+  }
   if (P.policy_thr == 0) return POL_NONE;
   uint32_t last = x.pol & 0xFFu, hits = x.pol >> 8;
   if (id == last) {
