@@ -329,7 +329,7 @@ __device__ __forceinline__ void fault_process(const Params& P, Rep<NT>& x, uint3
 #define PXS_ABSORB9 1
 #endif
 #ifndef PXS_ABSORB_MAX
-#define PXS_ABSORB_MAX 3   // messages absorbed per trip
+#define PXS_ABSORB_MAX 2   // messages absorbed per trip (A/B: 2 > 3 > 4 > 6 on config 2)
 #endif
 #ifndef PXS_ABSORB_ABD
 #define PXS_ABSORB_ABD 0
