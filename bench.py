@@ -2,19 +2,23 @@
 committed slots/s, 1M Multi-Paxos clusters of 5 replicas with Drop/Slow fault
 injection per GPU (BASELINE config 2), on 1..8 GPUs.
 
-One bench "step" = one pass of the hot path over the whole batch = one kernel
-launch advancing every cluster of every rank by --sim-steps virtual steps.
+One bench "step" = one pass of the hot path over the whole batch: every
+cluster of every rank advances --sim-steps virtual steps (config 2: 400, as
+launches of 50 steps each).  With the driver's --warmup 5 --steps 20 the
+timed region is config 2's virtual steps 2,000-10,000: past the ~1,200-step
+ramp while clusters desynchronise, and ending at the config's 10,000 steps.
 Inputs (cluster state, mailboxes) are resident in HBM before the timed region.
 
-  python bench.py [--gpus N --steps K --warmup W] [--config 2|3|4]
+  python bench.py [--gpus N --steps K --warmup W] [--config 2|3|4|5]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
 
---config 3 (ABD + linearizability scan) and --config 4 (FGrid 3x3, leader crash,
-ephemeral leaders) print their own lines; the default is the headline config 2.
+--config 3 (ABD + linearizability scan), 4 (FGrid 3x3, leader crash at the
+first timed step, re-election at zone 2) and 5 (WPaxos) print their own lines.
 Multi-GPU: see paxi_amd/dist.py — clusters shard by range, no data-path
 collective; RCCL all-reduces the statistics and the max time.
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -35,6 +39,14 @@ ALG_BYTES = {"P2a": 160, "P2b": 144, "P3": 192, "P1a": 64, "P1b": 64, "Request":
 ALG_BYTES_PER_COMMIT = 64
 
 METRIC = "sim messages delivered/sec + committed slots/sec, 1M Paxos clusters, 1-8 GPU"
+FLAG_NAMES = ("WOVF", "GHOST", "MBOX_OVF", "PEND_OVF", "UNFAITHFUL", "POISON", "BALLOT_OVF", "HIST_OVF")
+
+# per-config defaults: clusters per GPU, virtual steps per bench step, window, mailbox capacity
+DEFAULTS = {2: dict(clusters=1 << 20, sim_steps=400, window=16, mbox=32),
+            3: dict(clusters=1 << 20, sim_steps=80, window=16, mbox=16),
+            4: dict(clusters=1 << 19, sim_steps=200, window=16, mbox=24),
+            5: dict(clusters=1 << 18, sim_steps=200, window=16, mbox=24)}
+LAUNCH_STEPS = 50   # virtual steps fused per kernel launch
 
 
 def alg_bytes(delta):
@@ -48,12 +60,22 @@ def stats_delta(a, b):
     return d
 
 
+def build_id():
+    """Fingerprint of the HIP product sources and flags (what a traffic record was measured on)."""
+    import __graft_entry__ as ge
+    h = hashlib.sha256(" ".join(ge.HIP_FLAGS).encode())
+    for f in sorted(set(ge.HIP_SOURCES + ge.HIP_HEADERS)):
+        with open(os.path.join(ROOT, ge.CSRC, f), "rb") as fh:
+            h.update(f.encode() + fh.read())
+    return h.hexdigest()[:16]
+
+
 def workload(cfg_id, clusters, base, device, args):
     """(cfg, workload, fault process, scripted faults, description) of a BASELINE config."""
     from paxi_amd import abi
     if cfg_id == 2:
         cfg = abi.make_config(npz=[5], clusters=clusters, cluster_base=base, seed=42, window=args.window,
-                              mbox_cap=args.mbox, max_delay=4, steps_per_launch=args.sim_steps, device=device)
+                              mbox_cap=args.mbox, max_delay=4, steps_per_launch=LAUNCH_STEPS, device=device)
         wl = abi.make_workload(outstanding=8, target=0)
         fp = abi.make_fault_process(drop_ppm=1000, drop_len=50, slow_ppm=1000, slow_len=50, slow_min=1, slow_max=4)
         return cfg, wl, fp, [], {
@@ -62,25 +84,32 @@ def workload(cfg_id, clusters, base, device, args):
             "slow": "p=1e-3/step/link, 1-4 steps, 50-step windows"}
     if cfg_id == 3:
         cfg = abi.make_config(protocol=abi.ABD, npz=[5], clusters=clusters, cluster_base=base, seed=42, keys=16,
-                              mbox_cap=args.mbox, max_delay=4, steps_per_launch=args.sim_steps, device=device,
+                              mbox_cap=args.mbox, max_delay=4, steps_per_launch=LAUNCH_STEPS, device=device,
                               history=args.history)
         wl = abi.make_workload(outstanding=4, target=[0, 1, 2, 3], write_ppm=500_000)
         return cfg, wl, None, [], {
             "workload": "BASELINE config 3: ABD 5 replicas x 1M clusters/GPU, 16 keys, 50% writes, "
                         "linearizability scan on device", "replicas": 5, "outstanding": 4}
     if cfg_id == 4:
+        # Clients talk to leader 1.1 (replica 0) until it crashes for good at
+        # crash_step; from then on a second set of clients talks to 2.1
+        # (replica 3), whose first request runs phase 1 under -ephemeral_leader
+        # (paxos/replica.go:61) and re-elects it.  The first set stays blocked on
+        # the crashed leader: Paxi's HTTP client has no retry.
+        c = args.crash_step
         cfg = abi.make_config(npz=[3, 3, 3], clusters=clusters, cluster_base=base, seed=42, q1=abi.Q_FGRID_Q1,
-                              q2=abi.Q_FGRID_Q2, fz=1, ephemeral_leader=1, window=args.window, mbox_cap=24,
-                              max_delay=0, steps_per_launch=args.sim_steps, device=device)
-        wl = abi.make_workload(outstanding=4, target=[0, 0, 3, 3])
-        faults = [abi.make_fault(abi.FAULT_CRASH, 0, step_from=args.crash_step)]
+                              q2=abi.Q_FGRID_Q2, fz=1, ephemeral_leader=1, window=args.window, mbox_cap=args.mbox,
+                              max_delay=0, steps_per_launch=LAUNCH_STEPS, device=device)
+        wl = abi.make_workload(outstanding=8, target=[0, 0, 0, 0, 3, 3, 3, 3], start_step=[0, 0, 0, 0, c, c, c, c])
+        faults = [abi.make_fault(abi.FAULT_CRASH, 0, step_from=c)]
         return cfg, wl, None, faults, {
-            "workload": "BASELINE config 4: FGrid 3x3 (fz=1) x 512K clusters/GPU, ephemeral leaders, "
-                        f"leader 1.1 crashed at step {args.crash_step}", "replicas": 9, "outstanding": 4}
+            "workload": "BASELINE config 4: FGrid 3x3 (fz=1) x 512K clusters/GPU; leader 1.1 crashes for good at "
+                        f"step {c}, clients then turn to 2.1 which re-elects itself (ephemeral leader)",
+            "replicas": 9, "outstanding": "4 -> 1.1 from step 0, 4 -> 2.1 from the crash", "crash_step": c}
     if cfg_id == 5:
         cfg = abi.make_config(protocol=abi.WPAXOS, npz=[3, 3, 3], keys=8, fz=0, adaptive=1, policy_threshold=3,
-                              clusters=clusters, cluster_base=base, seed=42, window=args.window, mbox_cap=24,
-                              max_delay=0, steps_per_launch=args.sim_steps, device=device)
+                              clusters=clusters, cluster_base=base, seed=42, window=args.window, mbox_cap=args.mbox,
+                              max_delay=0, steps_per_launch=LAUNCH_STEPS, device=device)
         wl = abi.make_workload(outstanding=9, target=list(range(9)), locality_ppm=700_000)
         return cfg, wl, None, [], {
             "workload": "BASELINE config 5: WPaxos 3 zones x 3 nodes, 8 keys (kpaxos instances) per cluster, "
@@ -89,11 +118,14 @@ def workload(cfg_id, clusters, base, device, args):
     raise SystemExit(f"unknown config {cfg_id}")
 
 
-def measured_traffic(args, kernel, mbox):
-    """HBM bytes per launch of this exact workload from the PMC passes of
-    tools/traffic.sh (committed as profiles/traffic_config<c>.json).  The
-    simulation is seeded, so a launch moves the same bytes in every run of the
-    same workload; counters cannot be read from inside this process."""
+def measured_traffic(args, kernel, mbox, bid):
+    """HBM bytes per launch from the PMC passes of tools/traffic.sh (committed as
+    profiles/traffic_config<c>.json), attached when the record was measured on
+    this build (source fingerprint) and this workload (kernel, clusters, window,
+    mailbox, launch size).  The simulation is seeded, so a launch at a given
+    simulated step moves the same bytes in every run; the record names the
+    bench window (warmup, steps) it averaged.  Counters cannot be read from
+    inside this process."""
     path = os.path.join(ROOT, "profiles", f"traffic_config{args.config}.json")
     try:
         t = json.load(open(path))
@@ -101,31 +133,76 @@ def measured_traffic(args, kernel, mbox):
         return None
     same = (t.get("kernel") == kernel and t.get("clusters_per_gpu") == args.clusters
             and t.get("sim_steps_per_step") == args.sim_steps and t.get("window") == args.window
-            and t.get("mbox_cap") == mbox and t.get("steps") == args.steps and t.get("warmup") == args.warmup)
+            and t.get("mbox_cap") == mbox and t.get("build_id") == bid)
     if not same:
         return None
-    return {"bytes_per_launch": t["bytes_per_launch"], "source": os.path.relpath(path, ROOT)}
+    return {"bytes_per_launch": t["bytes_per_launch"], "source": os.path.relpath(path, ROOT),
+            "window": {"warmup": t.get("warmup"), "steps": t.get("steps")}}
 
 
-def cpu_baseline(args):
-    """The C oracle (same delivery schedule) on a bounded sample of the same workload."""
+def cpu_threads():
+    """Host threads for the CPU baseline: the CPUs this process may run on
+    (sched_getaffinity), capped by a cgroup CPU quota when one is set;
+    PAXISIM_CPU_THREADS overrides."""
+    if os.environ.get("PAXISIM_CPU_THREADS"):
+        return int(os.environ["PAXISIM_CPU_THREADS"]), "PAXISIM_CPU_THREADS"
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    why = f"sched_getaffinity ({n} of os.cpu_count() {os.cpu_count()})"
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if quota != "max":
+            q = max(1, int(int(quota) / int(period)))
+            if q < n:
+                n, why = q, f"cgroup cpu.max quota {quota}/{period}"
+    except (OSError, ValueError):
+        pass
+    return n, why
+
+
+def host_physical_cores():
+    """Physical cores of the host (sockets x cores per socket), from sysfs topology."""
+    try:
+        ids = set()
+        base = "/sys/devices/system/cpu"
+        for d in os.listdir(base):
+            if d.startswith("cpu") and d[3:].isdigit():
+                t = os.path.join(base, d, "topology")
+                ids.add((open(os.path.join(t, "physical_package_id")).read().strip(),
+                         open(os.path.join(t, "core_id")).read().strip()))
+        return len(ids) or None
+    except OSError:
+        return None
+
+
+def cpu_baseline(args, min_s=3.0):
+    """The C oracle (same delivery schedule) over exactly the GPU leg's timed
+    window of virtual steps, after the same warm-up: one thread on 256
+    clusters, then all usable host threads on enough clusters for >= min_s
+    seconds (the rate changes along a run, so the window must match)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    cfg, wl, fp, faults, _ = workload(args.config, args.cpu_clusters, 0, 0, args)
+    threads, why = cpu_threads()
+    warm, window = args.warmup * args.sim_steps, args.steps * args.sim_steps
     out = {}
+    clusters = 256
     for nthr in (1, threads):
+        cfg, wl, fp, faults, _ = workload(args.config, clusters, 0, 0, args)
         o = oracle_lib.OracleSim(cfg, wl, fp, faults)
-        o.step(args.warmup * args.sim_steps, threads=nthr)     # same warm-up as the GPU leg
+        o.step(warm, threads=nthr)
         s0 = o.stats().as_dict()
         t0 = time.perf_counter()
-        o.step(args.cpu_steps, threads=nthr)
+        o.step(window, threads=nthr)
         dt = time.perf_counter() - t0
         s1 = o.stats().as_dict()
-        out[nthr] = ((s1["delivered_total"] - s0["delivered_total"]) / dt, (s1["commits"] - s0["commits"]) / dt, dt)
+        out[nthr] = ((s1["delivered_total"] - s0["delivered_total"]) / dt, (s1["commits"] - s0["commits"]) / dt,
+                     dt, clusters)
         o.close()
-    v, c, dt = out[threads]
-    v1, _, dt1 = out[1]
+        if nthr == 1:   # size the multi-thread sample for >= min_s seconds
+            clusters = int(256 * threads * max(1.0, min_s / max(dt, 1e-3)))
+        if threads == 1:
+            break
+    v, c, dt, cl = out[threads]
+    v1, _, dt1, cl1 = out[1]
     cpu = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -134,31 +211,40 @@ def cpu_baseline(args):
                 break
     except OSError:
         pass
-    return {"value": v, "unit": "messages/s", "cores": threads, "kind": "port", "commits_per_s": c,
-            "single_thread_value": v1,
-            "sample": (f"C oracle (oracle/oracle.c), config {args.config} on {args.cpu_clusters} clusters x "
-                       f"{args.cpu_steps} steps after {args.warmup * args.sim_steps} warm-up steps; {threads} threads "
-                       f"{dt:.1f}s, 1 thread {dt1:.1f}s ({v1:.3g} msg/s); CPU {cpu}; GOMAXPROCS n/a (no Go toolchain)")}
+    phys = host_physical_cores()
+    res = {"value": v, "unit": "messages/s", "cores": threads, "kind": "port", "commits_per_s": c,
+           "single_thread_value": v1, "host_cpus": os.cpu_count(), "host_physical_cores": phys,
+           "threads_from": why,
+           "sample": (f"C oracle (oracle/oracle.c), config {args.config}, virtual steps [{warm}, {warm + window}) "
+                      f"after the same warm-up as the GPU leg: {threads} threads on {cl} clusters ({dt:.1f}s), "
+                      f"1 thread on {cl1} clusters ({dt1:.1f}s, {v1:.3g} msg/s); CPU {cpu}; "
+                      f"GOMAXPROCS n/a (no Go toolchain)")}
+    if phys and phys > threads:
+        # not measured: this process may use only `threads` CPUs of the host
+        res["linear_estimate_all_physical_cores"] = v / threads * phys
+    return res
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
     ap.add_argument("--clusters", type=int, default=None, help="clusters per GPU (default: the config's)")
-    ap.add_argument("--sim-steps", type=int, default=50, help="virtual steps per bench step (per launch)")
-    ap.add_argument("--window", type=int, default=16)
-    ap.add_argument("--mbox", type=int, default=16)
+    ap.add_argument("--sim-steps", type=int, default=None, help="virtual steps per bench step")
+    ap.add_argument("--window", type=int, default=None)
+    ap.add_argument("--mbox", type=int, default=None)
     ap.add_argument("--history", type=int, default=512, help="config 3: ops recorded per replica")
-    ap.add_argument("--crash-step", type=int, default=1000, help="config 4: step of the leader crash")
-    ap.add_argument("--cpu-clusters", type=int, default=16384)
-    ap.add_argument("--cpu-steps", type=int, default=1600)
+    ap.add_argument("--crash-step", type=int, default=None,
+                    help="config 4: step of the leader crash (default: the first timed step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
-    if args.clusters is None:
-        args.clusters = {2: 1 << 20, 3: 1 << 20, 4: 1 << 19, 5: 1 << 18}[args.config]
+    for k, v in DEFAULTS[args.config].items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
+    if args.crash_step is None:
+        args.crash_step = args.warmup * args.sim_steps
 
     import torch
     import torch.distributed as dist
@@ -223,7 +309,9 @@ def main():
         occ = sim.occupancy()
         desc.update({"tiles_per_cu": occ[0], "lds_per_tile": occ[1], "staged_msgs": occ[2]})
         desc.update({"clusters_per_gpu": args.clusters, "sim_steps_per_step": args.sim_steps,
+                     "timed_sim_steps": [args.warmup * args.sim_steps, (args.warmup + args.steps) * args.sim_steps],
                      "window": args.window, "mbox_cap": cfg.mbox_cap, "parallelism": f"cluster-sharded x{world}"})
+        bid = build_id()
         out = {
             "metric": METRIC,
             "value": tot["delivered_total"] / dt_max,
@@ -241,21 +329,26 @@ def main():
             "commits_per_s": tot["commits"] / dt_max,
             "sim_steps_per_s": args.sim_steps * args.steps / dt_max,
             "agreement_violations": int(tot["violations"]),
-            "unfaithful_clusters": int(tot["unfaithful"]),
-            "poisoned_clusters": int(tot["poisoned"]),
+            "unfaithful_clusters": int(tot["flag_UNFAITHFUL"]),
+            "poisoned_clusters": int(tot["flag_POISON"]),
+            "flagged_clusters": {n: int(tot["flag_" + n]) for n in FLAG_NAMES},
+            "clusters_total": args.clusters * world,
             "kernel_ms_per_step": kms_max / args.steps,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": f"sim_steps<{abi.n_replicas(cfg)},{proto}>",
-                         "avg_launch_ms": avg_launch_ms, "alg_bytes_per_launch": alg_bytes(d) / max(1, launches)},
+                         "avg_launch_ms": avg_launch_ms, "launches": launches,
+                         "alg_bytes_per_launch": alg_bytes(d) / max(1, launches)},
+            "build_id": bid,
         }
-        tr = measured_traffic(args, out["roofline"]["kernel"], cfg.mbox_cap)
+        tr = measured_traffic(args, out["roofline"]["kernel"], cfg.mbox_cap, bid)
         if tr is not None:
             out["roofline"]["traffic"] = tr["bytes_per_launch"]
             out["roofline"]["traffic_source"] = tr["source"]
+            out["roofline"]["traffic_window"] = tr["window"]
         if lin is not None:
             out["linearizability"] = lin
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
     sim.close()

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PAXISIM_ABI_VERSION 5
+#define PAXISIM_ABI_VERSION 6
 
 #define PAXISIM_MAX_N        16  /* replicas per cluster (ack masks are u16) */
 #define PAXISIM_MAX_ZONES    16
@@ -171,6 +171,9 @@ typedef struct paxisim_workload {
   uint32_t conflicts;         /* CONFLICT: percent of commands on key 0 (Bconfig.Conflicts) */
   uint32_t key_cdf[PAXISIM_MAX_KEYS]; /* TABLE: key = #{k < keys-1 : u32 draw >= key_cdf[k]};
                                  non-decreasing over [0, keys-1) */
+  uint32_t start_step[PAXISIM_MAX_WORKERS]; /* step at which worker w's first request reaches
+                                 target[w] (0 = at creation): e.g. clients that turn to
+                                 another replica after a crash (BASELINE config 4) */
 } paxisim_workload;
 
 /* Random fault process, applied per (cluster, src, dst) link every step. */
@@ -242,6 +245,23 @@ typedef struct paxisim_stats {
   uint64_t flagged[8];        /* clusters with flag bit i set */
 } paxisim_stats;
 
+/* One log entry (read_log): paxos/paxos.go:11-18 entry of a slot in the
+ * replica's window [execute, execute + W). */
+#define PAXISIM_LOG_EXISTS  0x1u  /* p.log[slot] != nil */
+#define PAXISIM_LOG_COMMIT  0x2u  /* entry.commit */
+#define PAXISIM_LOG_QUORUM  0x4u  /* entry.quorum != nil (created by P2a / re-proposed) */
+#define PAXISIM_LOG_REQUEST 0x8u  /* entry.request != nil */
+#define PAXISIM_LOG_HELD    0x10u /* slot inside the window (else the fields are 0) */
+typedef struct paxisim_log_entry {
+  uint64_t ballot;            /* entry.ballot (64-bit Ballot) */
+  int32_t  slot;
+  uint32_t cmd;               /* command id */
+  uint32_t flags;             /* PAXISIM_LOG_* */
+  uint32_t acks;              /* entry.quorum ack mask (replica indices) */
+  uint32_t request;           /* command id | origin << 27 (origin PAXISIM_CLIENT_SRC = HTTP), or 0 */
+  uint32_t pad;
+} paxisim_log_entry;
+
 typedef struct paxisim paxisim;   /* opaque handle */
 
 int  paxisim_abi_version(void);
@@ -260,6 +280,14 @@ int  paxisim_fault_add(paxisim* h, const paxisim_fault* f);
 int  paxisim_step(paxisim* h, uint32_t nsteps);
 int  paxisim_sync(paxisim* h);
 
+/* The HTTP request path (http.go:99, handleRoot puts the request straight on
+ * MessageChan): a client request for command `cid` reaches `replica` of local
+ * cluster `cluster` in the next step run (paxisim_step).  The closed-loop
+ * workers own cids 1 + w + outstanding*j; an injected cid outside that set is
+ * an external client whose reply reaches no worker.  EINVAL if the replica's
+ * client mailbox for that step is full. */
+int  paxisim_inject(paxisim* h, uint64_t cluster, uint32_t replica, uint32_t cid);
+
 /* Totals over the handle. */
 int  paxisim_stats_get(paxisim* h, paxisim_stats* out);
 
@@ -273,6 +301,11 @@ int  paxisim_read_state(paxisim* h, uint64_t cluster_lo, uint64_t n,
  * then key. */
 int  paxisim_read_instances(paxisim* h, uint64_t cluster_lo, uint64_t n,
                             paxisim_instance_state* out);
+
+/* Log entries of slots [slot_lo, slot_lo + n) of one Paxos instance (replica;
+ * WPaxos: the kpaxos of `key`) of local cluster `cluster`. */
+int  paxisim_read_log(paxisim* h, uint64_t cluster, uint32_t replica, uint32_t key, int32_t slot_lo,
+                      uint32_t n, paxisim_log_entry* out);
 
 /* Agreement scan (client.go:279-320 / tla Safety): number of clusters in
  * which two replicas executed different commands in the same slot (of the

@@ -121,6 +121,9 @@ int oracle_quorum(uint32_t kind, uint32_t fz, uint32_t n_zones, const uint32_t* 
 /* Simulation state                                                          */
 /* ------------------------------------------------------------------------ */
 typedef struct { uint32_t hdr, ballot, slot, cid; } rec_t;   /* 16-B message record */
+/* an entry re-created below execute: slot, ballot, commit, live while t < until */
+typedef struct { uint32_t slot, ballot, commit, until; } ghost_t;
+#define GMAX 8
 #define HDR(type, n) ((uint32_t)(type) | ((uint32_t)(n) << 8))
 #define HDR_TYPE(h) ((h) & 0xFFu)
 #define HDR_N(h) (((h) >> 8) & 0xFFu)
@@ -176,8 +179,8 @@ typedef struct inst {
   uint32_t pol_n[PAXISIM_MAX_N], pol_sum, pol_time, pol_zone;
   double pol_s;
   uint32_t iflags;                 /* WOVF / GHOST raised on this instance's log */
-  /* Uncommitted ghost entries Go would hold below execute: slot range and ballot range */
-  uint32_t glo, ghi, gmin, gmax;
+  /* Entries Go holds below execute ("ghosts"), while they can still be observed */
+  ghost_t ghost[GMAX];
 } inst_t;
 
 typedef struct replica {
@@ -224,6 +227,7 @@ struct oracle_sim {
   uint32_t OW;                     /* ABD op table size */
   uint32_t NK;                     /* Paxos instances per replica: WPaxos keys, else 1 */
   uint32_t q1, q2;                 /* quorum kinds in use (WPaxos: from fz, wpaxos/kpaxos.go:16-28) */
+  uint32_t late_workers;           /* some worker has start_step > 0 */
 };
 
 /* handler context: one replica of one cluster at one step */
@@ -411,23 +415,66 @@ static inline int is_leader(const ctx_t* x) {             /* Paxos.IsLeader paxo
   return x->p->active || bal_id(x->p->ballot) == x->r;
 }
 
-/* An entry Go would create or update below execute (a "ghost": update() or
- * HandleP2a on a slot already executed here) is not stored.  A ghost is inert
- * except to HandleP2b (paxos.go:270-310), which for m.Ballot >= e.ballot
- * adopts a higher ballot or, on m.Ballot == e.ballot owned by self, panics on
- * the nil quorum; the summary below makes that observation detectable. */
-static void ghost(ctx_t* x, int32_t s, uint32_t b) {
-  inst_t* p = x->p;
-  raise_flag(x, PAXISIM_F_GHOST);
-  if ((uint32_t)s < p->glo) p->glo = (uint32_t)s;
-  if ((uint32_t)s > p->ghi) p->ghi = (uint32_t)s;
-  if (b < p->gmin) p->gmin = b;
-  if (b > p->gmax) p->gmax = b;
+/* Entries below execute ("ghosts").  exec() deletes an executed entry
+ * (paxos.go:366), but update() (173-177), HandleP2a (254-258) and HandleP3
+ * (326) re-create one when a message for an executed slot arrives, and Go
+ * keeps it forever.  Such an entry is read only by HandleP2b (270-310): a P2b
+ * for the slot adopts a higher ballot, or panics on the nil quorum when the
+ * ballot is this replica's own and equals the entry's.  A P2b for slot s
+ * reaches replica r only as the answer to a P2a(s) r sent while s >= execute,
+ * so it arrives at most 2 + 2*max_delay steps after r executed s: a ghost is
+ * kept for that long after it is (re)created and then forgotten.  Within that
+ * life the table is exact; a full table raises UNFAITHFUL. */
+static inline uint32_t ghost_life(const ctx_t* x) { return 3u + 2u * x->s->cfg.max_delay; }
+static ghost_t* ghost_find(ctx_t* x, int32_t s) {
+  uint32_t i;
+  for (i = 0; i < GMAX; i++) {
+    ghost_t* g = &x->p->ghost[i];
+    if (g->until > x->t && g->slot == (uint32_t)s) return g;
+  }
+  return NULL;
 }
-static int ghost_observed(const ctx_t* x, int32_t ms, uint32_t mb) {
-  const inst_t* p = x->p;
-  if ((uint32_t)ms < p->glo || (uint32_t)ms > p->ghi || mb < p->gmin) return 0;
-  return mb > p->ballot || (bal_id(mb) == x->r && mb <= p->gmax);
+static ghost_t* ghost_alloc(ctx_t* x, int32_t s) {
+  uint32_t i;
+  raise_flag(x, PAXISIM_F_GHOST);
+  for (i = 0; i < GMAX; i++) {
+    ghost_t* g = &x->p->ghost[i];
+    if (g->until <= x->t) {
+      g->slot = (uint32_t)s; g->ballot = 0; g->commit = 0; g->until = x->t + ghost_life(x);
+      return g;
+    }
+  }
+  raise_flag(x, PAXISIM_F_UNFAITHFUL);                     /* cannot keep this ghost */
+  return NULL;
+}
+/* update() / HandleP2a on a slot below execute: create, or raise an uncommitted ballot */
+static void ghost(ctx_t* x, int32_t s, uint32_t b) {
+  ghost_t* g = ghost_find(x, s);
+  if (g) {
+    if (!g->commit && b > g->ballot) g->ballot = b;
+    return;
+  }
+  if ((g = ghost_alloc(x, s))) g->ballot = b;
+}
+/* HandleP3 on a slot below execute: the entry exists and is committed (326-331) */
+static void ghost_commit(ctx_t* x, int32_t s) {
+  ghost_t* g = ghost_find(x, s);
+  if (!g) g = ghost_alloc(x, s);
+  if (g) g->commit = 1;
+}
+/* HandleP2b (270-310) for a slot below execute */
+static void ghost_p2b(ctx_t* x, int32_t ms, uint32_t mb) {
+  inst_t* p = x->p;
+  ghost_t* g = ghost_find(x, ms);
+  if (!g || mb < g->ballot || g->commit) return;           /* !exist || m.Ballot < e.ballot || e.commit */
+  if (mb > p->ballot) {
+    p->ballot = mb;
+    p->active = 0;
+  }
+  if (bal_id(mb) == x->r && mb == g->ballot) {             /* nil quorum: Go panics */
+    raise_flag(x, PAXISIM_F_POISON);
+    x->stop = 1;
+  }
 }
 
 static void paxos_forward(ctx_t* x) {                     /* paxos.go:371-376 */
@@ -610,8 +657,8 @@ static void paxos_handle_p2b(ctx_t* x, uint32_t src, uint32_t mb, int32_t ms) { 
   inst_t* p = x->p;
   entry_t* e;
   if (!in_window(x, ms)) {
-    if (ms < p->execute ? ghost_observed(x, ms, mb) : (x->p->iflags & PAXISIM_F_WOVF) != 0)
-      raise_flag(x, PAXISIM_F_UNFAITHFUL);
+    if (ms < p->execute) ghost_p2b(x, ms, mb);
+    else if (x->p->iflags & PAXISIM_F_WOVF) raise_flag(x, PAXISIM_F_UNFAITHFUL);
     return;
   }
   e = log_at(x, ms);
@@ -663,7 +710,7 @@ static void paxos_handle_p3(ctx_t* x, uint32_t mb, int32_t ms, uint32_t mcid) { 
       return;
     }
   } else if (ms < p->execute) {
-    raise_flag(x, PAXISIM_F_GHOST);
+    ghost_commit(x, ms);
   } else {
     raise_flag(x, PAXISIM_F_WOVF);
   }
@@ -1029,6 +1076,26 @@ static void fault_process(ctx_t* x) {
   }
 }
 
+/* A worker whose first request is due at step t sends it to its target now
+ * (paxisim_workload.start_step); it joins the target's client queue after the
+ * requests already there. */
+static void client_start(ctx_t* x) {
+  const struct oracle_sim* s = x->s;
+  uint32_t w;
+  for (w = 0; w < s->wl.outstanding; w++) {
+    uint8_t* cnt;
+    rec_t* m;
+    if (s->wl.start_step[w] != x->t || x->t == 0 || s->wl.target[w] != x->r) continue;
+    x->c->wk_cur[w] = 1u + w;
+    x->c->wk_issued[w] = 1;
+    cnt = mb_cnt(s, x->c, x->t % s->D, x->r, s->N);
+    if (*cnt >= s->M) { raise_flag(x, PAXISIM_F_MBOX_OVF | PAXISIM_F_UNFAITHFUL); continue; }
+    m = mb_rec(s, x->c, x->t % s->D, x->r, s->N, *cnt);
+    m->hdr = HDR(PAXISIM_MSG_REQUEST, 0); m->ballot = 0; m->slot = 0; m->cid = 1u + w;
+    (*cnt)++;
+  }
+}
+
 static void replica_step(const struct oracle_sim* s, cluster_t* c, uint32_t r, uint32_t t) {
   ctx_t x;
   uint32_t b = t % s->D, src, rem[PAXISIM_MAX_N + 1], pos[PAXISIM_MAX_N + 1], total = 0, i;
@@ -1037,6 +1104,7 @@ static void replica_step(const struct oracle_sim* s, cluster_t* c, uint32_t r, u
   x.r = r; x.t = t; x.stop = 0;
   x.hs = step_key(c->kc, t);
   x.n->send_seq = 0;
+  if (s->late_workers) client_start(&x);
   fault_process(&x);
   crash = crashed(s, c, r, t);
   for (src = 0; src < s->NS; src++) {
@@ -1143,7 +1211,6 @@ static void cluster_init(struct oracle_sim* s, cluster_t* c, uint64_t gid, entry
       p->log = logs + ((size_t)r * s->NK + k) * s->W;
       p->exists = s->cfg.protocol != PAXISIM_WPAXOS;
       p->pol_last = POL_NONE;
-      p->glo = p->gmin = 0xFFFFFFFFu;
     }
     if (s->cfg.protocol == PAXISIM_ABD) {
       c->rep[r].kv_val = (uint32_t*)calloc(2u * s->cfg.keys, sizeof(uint32_t));
@@ -1158,6 +1225,7 @@ static void cluster_init(struct oracle_sim* s, cluster_t* c, uint64_t gid, entry
   for (w = 0; w < s->wl.outstanding; w++) {
     uint32_t tg = s->wl.target[w];
     uint8_t* cnt = mb_cnt(s, c, 0, tg, s->N);
+    if (s->wl.start_step[w]) continue;                     /* joins later (client_start) */
     rec_t* m = mb_rec(s, c, 0, tg, s->N, *cnt);
     m->hdr = HDR(PAXISIM_MSG_REQUEST, 0); m->ballot = 0; m->slot = 0; m->cid = 1u + w;
     (*cnt)++;
@@ -1189,6 +1257,7 @@ int oracle_create(const paxisim_config* cfg, const paxisim_workload* wl,
   }
   s->C = cfg->clusters;
   s->keep_xlog = cfg->clusters <= 16;
+  for (z = 0; z < s->wl.outstanding; z++) s->late_workers |= s->wl.start_step[z] != 0;
   s->OW = abd_ow(wl->outstanding);
   s->NK = cfg->protocol == PAXISIM_WPAXOS ? cfg->keys : 1u;
   s->q1 = cfg->q1;
@@ -1248,6 +1317,51 @@ int oracle_destroy(oracle_sim* s) {
   }
   free(s->cl);
   free(s);
+  return 0;
+}
+
+static uint64_t expand_ballot(const struct oracle_sim* s, uint32_t b);
+
+/* The HTTP request path (http.go:99): client request `cid` reaches replica r
+ * of cluster cl in the next step (paxisim_inject). */
+int oracle_inject(oracle_sim* s, uint64_t cl, uint32_t r, uint32_t cid) {
+  cluster_t* c;
+  uint8_t* cnt;
+  rec_t* m;
+  if (!s || cl >= s->C || r >= s->N || cid < 1 || cid > CID_MAX) return fail(PAXISIM_EINVAL, "bad inject");
+  c = &s->cl[cl];
+  cnt = mb_cnt(s, c, s->t % s->D, r, s->N);
+  if (*cnt >= s->M) return fail(PAXISIM_EINVAL, "client mailbox full");
+  m = mb_rec(s, c, s->t % s->D, r, s->N, *cnt);
+  m->hdr = HDR(PAXISIM_MSG_REQUEST, 0); m->ballot = 0; m->slot = 0; m->cid = cid;
+  (*cnt)++;
+  return 0;
+}
+
+int oracle_read_log(oracle_sim* s, uint64_t cl, uint32_t r, uint32_t key, int32_t lo, uint32_t n,
+                    paxisim_log_entry* out) {
+  const inst_t* p;
+  uint32_t i;
+  if (!s || !out || cl >= s->C || r >= s->N || key >= s->NK) return fail(PAXISIM_EINVAL, "bad argument");
+  p = &s->cl[cl].rep[r].inst[key];
+  for (i = 0; i < n; i++) {
+    const int32_t sl = lo + (int32_t)i;
+    paxisim_log_entry* o = &out[i];
+    memset(o, 0, sizeof *o);
+    o->slot = sl;
+    if (sl < p->execute || sl >= p->execute + (int32_t)s->W) continue;
+    {
+      const entry_t* e = &p->log[(uint32_t)sl & (s->W - 1u)];
+      o->flags = PAXISIM_LOG_HELD;
+      if (!(e->meta & E_EXISTS)) continue;
+      o->flags |= PAXISIM_LOG_EXISTS | (e->meta & E_COMMIT ? PAXISIM_LOG_COMMIT : 0u) |
+                  (e->meta & E_QUORUM ? PAXISIM_LOG_QUORUM : 0u) | (e->req ? PAXISIM_LOG_REQUEST : 0u);
+      o->ballot = expand_ballot(s, e->ballot);
+      o->cmd = e->cmd;
+      o->acks = E_ACK(e->meta);
+      o->request = e->req;
+    }
+  }
   return 0;
 }
 

@@ -6,7 +6,7 @@ structs, so the two speak exactly the same ABI.
 """
 import ctypes as C
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 MAX_N = 16
 MAX_ZONES = 16
 MAX_WORKERS = 32
@@ -88,6 +88,7 @@ class Workload(C.Structure):
         ("distribution", C.c_uint32),
         ("conflicts", C.c_uint32),
         ("key_cdf", C.c_uint32 * MAX_KEYS),
+        ("start_step", C.c_uint32 * MAX_WORKERS),
     ]
 
 
@@ -144,6 +145,20 @@ class InstanceState(C.Structure):
                 self.npending, self.digest, self.policy_last, self.policy_hits, tuple(self.policy_state))
 
 
+LOG_EXISTS, LOG_COMMIT, LOG_QUORUM, LOG_REQUEST, LOG_HELD = 0x1, 0x2, 0x4, 0x8, 0x10
+
+
+class LogEntry(C.Structure):
+    """One paxos/paxos.go:11-18 entry of a replica's window (read_log)."""
+    _fields_ = [
+        ("ballot", C.c_uint64), ("slot", C.c_int32), ("cmd", C.c_uint32), ("flags", C.c_uint32),
+        ("acks", C.c_uint32), ("request", C.c_uint32), ("pad", C.c_uint32),
+    ]
+
+    def as_tuple(self):
+        return (self.ballot, self.slot, self.cmd, self.flags, self.acks, self.request)
+
+
 class Stats(C.Structure):
     _fields_ = [
         ("steps", C.c_uint64), ("clusters", C.c_uint64),
@@ -175,6 +190,8 @@ def declare(lib, prefix):
         "read_state": (C.c_int, [h, C.c_uint64, C.c_uint64, P(ReplicaState)]),
         "read_instances": (C.c_int, [h, C.c_uint64, C.c_uint64, P(InstanceState)]),
         "check": (C.c_int, [h, P(C.c_uint64)]),
+        "inject": (C.c_int, [h, C.c_uint64, C.c_uint32, C.c_uint32]),
+        "read_log": (C.c_int, [h, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int32, C.c_uint32, P(LogEntry)]),
         "last_error": (C.c_char_p, []),
     }
     for name, (res, args) in spec.items():
@@ -205,7 +222,7 @@ def make_config(npz=(5,), protocol=PAXOS, q1=Q_MAJORITY, q2=Q_MAJORITY, fz=0, th
 
 
 def make_workload(outstanding=1, max_requests=0, write_ppm=1_000_000, locality_ppm=0, target=0,
-                  distribution="uniform", keys=None, **dist_params):
+                  distribution="uniform", keys=None, start_step=0, **dist_params):
     """Closed-loop workload.  `distribution` is a Bconfig.Distribution name
     (benchmark.go:202-233, see paxi_amd.workload); the table distributions
     ("normal", "zipfan", "exponential") need the cluster's `keys`."""
@@ -214,6 +231,7 @@ def make_workload(outstanding=1, max_requests=0, write_ppm=1_000_000, locality_p
     w.outstanding, w.max_requests, w.write_ppm, w.locality_ppm = outstanding, max_requests, write_ppm, locality_ppm
     for i in range(MAX_WORKERS):
         w.target[i] = target[i % len(target)] if isinstance(target, (list, tuple)) else target
+        w.start_step[i] = start_step[i % len(start_step)] if isinstance(start_step, (list, tuple)) else start_step
     _wl.set_distribution(w, distribution, keys, **dist_params)
     return w
 

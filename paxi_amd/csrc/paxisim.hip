@@ -13,11 +13,9 @@
 #include <utility>
 #include <vector>
 
-#include "abd_kernel.h"
 #include "lin_kernel.h"
 #include "paxisim_dev.h"
-#include "paxos_kernel.h"
-#include "wpaxos_kernel.h"
+#include "step_ops.h"
 
 using namespace pxs;
 
@@ -48,6 +46,8 @@ struct paxisim {
   size_t arena_bytes = 0;
   uint64_t* d_scratch = nullptr;   // reductions
   hipStream_t stream = nullptr;
+  StepOps ops{};
+  int lds_set = -1;                // dynamic-LDS ceiling set for ops on this handle's device
   uint32_t t = 0;
   uint32_t S = 32;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
@@ -92,6 +92,7 @@ __global__ void init_kernel(Params P) {
   uint32_t* wiss = reinterpret_cast<uint32_t*>(img + P.img.off_wiss);
   uint4* rec = P.rec + (size_t)blk * P.rec_per_block;
   for (uint32_t w = 0; w < P.WK; w++) {         // each worker's first request waits at step 0
+    if (P.start_step[w]) continue;              // joins later (client_start, sim_core.h)
     const uint32_t box = (0u * P.N + P.target[w]) * P.NS + P.N;
     const uint32_t k = cnt[(box << 6) | lane];
     rec[((box * P.M + k) << 6) | lane] = make_uint4(PAXISIM_MSG_REQUEST, 0u, 0u, 1u + w);
@@ -288,6 +289,64 @@ __global__ void check_kernel(Params P, uint64_t* out) {
   if ((threadIdx.x & 63) == 0 && bad) atomicAdd((unsigned long long*)out, (unsigned long long)bad);
 }
 
+// paxisim_inject: one client request record into (bucket b, dst r, src client)
+__global__ void inject_kernel(Params P, uint64_t c, uint32_t r, uint32_t b, uint32_t cid, uint32_t* status) {
+  if (threadIdx.x != 0) return;
+  const uint32_t blk = (uint32_t)(c / LANES), lane = (uint32_t)(c % LANES);
+  uint8_t* cnt = P.image + (size_t)blk * P.img.bytes + P.img.off_cnt;
+  const uint32_t box = (b * P.N + r) * P.NS + P.N;
+  const uint32_t k = cnt[(box << 6) | lane];
+  if (k >= P.M) {
+    *status = 1;
+    return;
+  }
+  P.rec[(size_t)blk * P.rec_per_block + (((box * P.M + k) << 6) | lane)] = make_uint4(PAXISIM_MSG_REQUEST, 0u, 0u, cid);
+  cnt[(box << 6) | lane] = (uint8_t)(k + 1u);
+  *status = 0;
+}
+
+// paxisim_read_log: one thread per slot of one instance's window
+__global__ void read_log_kernel(Params P, uint64_t c, uint32_t r, uint32_t key, int32_t lo, uint32_t n,
+                                paxisim_log_entry* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t blk = (uint32_t)(c / LANES), lane = (uint32_t)(c % LANES);
+  const int32_t s = lo + (int32_t)i;
+  paxisim_log_entry o;
+  memset(&o, 0, sizeof o);
+  o.slot = s;
+  int32_t execute;
+  uint32_t eb, ec, ea, ex;
+  const uint32_t w = (uint32_t)s & (P.W - 1u);
+  if (P.protocol == PAXISIM_WPAXOS) {
+    const size_t si = (((size_t)blk * P.keys + key) * P.N + r) * LANES + lane;
+    execute = (int32_t)P.wst[2 * si].z;
+    const uint32_t* e = P.wlog + (si * P.W + w) * 4u;
+    eb = e[0]; ec = e[1]; ea = e[2]; ex = e[3];
+  } else {
+    execute = (int32_t)P.execute[rc(P, r, c)];
+    const uint8_t* img = P.image + (size_t)blk * P.img.bytes;
+    const uint32_t li = ((r * P.W + w) << 6) | lane;
+    eb = reinterpret_cast<const uint32_t*>(img + P.img.off_a)[li];
+    ec = reinterpret_cast<const uint32_t*>(img + P.img.off_b)[li];
+    ea = reinterpret_cast<const uint32_t*>(img + P.img.off_c)[li];
+    ex = P.reqx[(size_t)blk * (P.N * P.W * LANES) + li];
+  }
+  if (s >= execute && s < execute + (int32_t)P.W) {
+    o.flags = PAXISIM_LOG_HELD;
+    if (ec & EF_EXISTS) {
+      o.flags |= PAXISIM_LOG_EXISTS | ((ec & EF_COMMIT) ? PAXISIM_LOG_COMMIT : 0u) |
+                 ((ec & EF_QUORUM) ? PAXISIM_LOG_QUORUM : 0u) |
+                 ((ec & (EF_REQSELF | EF_REQEXT)) ? PAXISIM_LOG_REQUEST : 0u);
+      o.ballot = eb;                                          // compressed; expanded on the host
+      o.cmd = ec & CMD_MASK;
+      o.acks = ea;
+      o.request = (ec & EF_REQSELF) ? ((ec & CMD_MASK) | (PAXISIM_CLIENT_SRC << 27)) : (ec & EF_REQEXT) ? ex : 0u;
+    }
+  }
+  out[i] = o;
+}
+
 // ---------------------------------------------------------------------------
 // C-ABI
 // ---------------------------------------------------------------------------
@@ -378,11 +437,10 @@ extern "C" int paxisim_destroy(paxisim* h) {
   return 0;
 }
 
-static hipError_t kernel_vgprs(const paxisim* h, int* v, int* maxthr);
-// stage_built<NT, Proto>() (sim_core.h) for the instance launch_any picks
-static bool stage_built_host(uint32_t protocol, uint32_t N) {
-  if (protocol == PAXISIM_ABD) return N == 3 || N == 5;
-  return N == 9;
+static StepOps step_ops_for(uint32_t protocol, uint32_t N) {
+  if (protocol == PAXISIM_WPAXOS) return wpaxos_step_ops(N);
+  if (protocol == PAXISIM_ABD) return abd_step_ops(N);
+  return paxos_step_ops(N);
 }
 
 extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload* wl, const paxisim_fault_process* fp,
@@ -470,7 +528,11 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
       h->node_of[r] = k + 1;
     }
   }
-  for (uint32_t w = 0; w < PAXISIM_MAX_WORKERS; w++) P.target[w] = wl->target[w];
+  for (uint32_t w = 0; w < PAXISIM_MAX_WORKERS; w++) {
+    P.target[w] = wl->target[w];
+    P.start_step[w] = w < wl->outstanding ? wl->start_step[w] : 0u;
+    if (P.start_step[w]) P.late_workers |= 1u << w;
+  }
 
   P.img = proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D);
   {
@@ -478,7 +540,8 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     // the step kernel's registers leave wave slots for on every SIMD
     // (ceil(G*N/4) <= waves per SIMD) and the LDS holds, at most 4.
     int vgprs = 0, maxthr = 0;
-    if (kernel_vgprs(h, &vgprs, &maxthr) != hipSuccess || vgprs <= 0) vgprs = 512;
+    h->ops = step_ops_for(P.protocol, N);
+    if (h->ops.attrs(&vgprs, &maxthr) != hipSuccess || vgprs <= 0) vgprs = 512;
     if (maxthr <= 0) maxthr = (int)(N * LANES);
     const uint32_t alloc = ((uint32_t)vgprs + 7u) / 8u * 8u;
     const uint32_t wps = alloc >= 512u ? 1u : (512u / alloc < 8u ? 512u / alloc : 8u);
@@ -492,7 +555,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     if (const char* e = getenv("PAXISIM_STAGE")) jmax = (uint32_t)atoi(e);   // tuning override
     const uint32_t room = (LDS_MAX / G - P.img.bytes) / (N * LANES * 16u);
     P.J = room < jmax ? room : jmax;
-    if (!stage_built_host(P.protocol, N)) P.J = 0;   // that instance has no staged loop
+    if (!h->ops.staged) P.J = 0;   // that instance has no staged loop
     P.off_stage = P.img.bytes;
     P.lds_bytes = P.img.bytes + P.J * N * LANES * 16u;
   }
@@ -511,7 +574,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     uint32_t* links = carve<uint32_t>(p, NC * N * 2);
     uint32_t* cke = carve<uint32_t>(p, NIC * CKR);
     uint64_t* ckd = carve<uint64_t>(p, NIC * CKR);
-    uint4* gst = carve<uint4>(p, NIC);
+    uint4* gst = carve<uint4>(p, NIC * GMAX);
     uint32_t* st = carve<uint32_t>(p, NC * NSTAT);
     uint32_t* reqx = carve<uint32_t>(p, wp ? 0 : NC * P.W);
     uint4* wst = carve<uint4>(p, wp ? NIC * 2 : 0);
@@ -580,100 +643,14 @@ extern "C" int paxisim_fault_add(paxisim* h, const paxisim_fault* f) {
   return 0;
 }
 
-template <int NT, class Proto>
-static hipError_t launch_steps(paxisim* h, uint32_t t0, uint32_t n) {
-  const Params& P = h->P;
-  const unsigned grid = (unsigned)(P.C / (LANES * P.G));
-  // The dynamic-LDS ceiling is set to what this launch uses, not to the CU's
-  // 160 KB: the runtime sizes every workgroup's LDS allocation by it, and a
-  // 160 KB ceiling would hold each CU to one resident workgroup.
-  static thread_local int attr_bytes = -1;
-  const int lds = (int)(P.G * P.lds_bytes);
-  if (attr_bytes != lds) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sim_steps<NT, Proto>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (e != hipSuccess) return e;
-    attr_bytes = lds;
-  }
-  sim_steps<NT, Proto><<<grid, P.G * P.N * LANES, (size_t)lds, h->stream>>>(P, t0, n);
-  return hipGetLastError();
-}
-
-// Workgroups of the step kernel resident per CU (diagnostic: hipOccupancy API).
-template <int NT, class Proto>
-static hipError_t occupancy(paxisim* h, int* blocks) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, reinterpret_cast<const void*>(&sim_steps<NT, Proto>),
-                                                      (int)(h->P.G * h->P.N * LANES),
-                                                      (size_t)h->P.G * h->P.lds_bytes);
-}
-// VGPRs of the step kernel (sizes the cluster groups per workgroup)
-template <int NT, class Proto>
-static hipError_t vgprs_of(int* v, int* maxthr) {
-  hipFuncAttributes a;
-  hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&sim_steps<NT, Proto>));
-  if (e == hipSuccess) {
-    *v = a.numRegs;
-    *maxthr = a.maxThreadsPerBlock;
-  }
-  return e;
-}
-static hipError_t kernel_vgprs(const paxisim* h, int* v, int* m) {
-#ifdef PXS_ONLY_PAXOS5
-  return vgprs_of<5, PaxosProto>(v, m);
-#else
-  const uint32_t N = h->P.N;
-  if (h->P.protocol == PAXISIM_WPAXOS) return N == 9 ? vgprs_of<9, WPaxosProto>(v, m) : vgprs_of<0, WPaxosProto>(v, m);
-  if (h->P.protocol == PAXISIM_ABD)
-    return N == 3 ? vgprs_of<3, AbdProto>(v, m) : N == 5 ? vgprs_of<5, AbdProto>(v, m) : vgprs_of<0, AbdProto>(v, m);
-  switch (N) {
-    case 3: return vgprs_of<3, PaxosProto>(v, m);
-    case 5: return vgprs_of<5, PaxosProto>(v, m);
-    case 9: return vgprs_of<9, PaxosProto>(v, m);
-    default: return vgprs_of<0, PaxosProto>(v, m);
-  }
-#endif
-}
-static hipError_t occupancy_any(paxisim* h, int* blocks) {
-#ifdef PXS_ONLY_PAXOS5
-  return occupancy<5, PaxosProto>(h, blocks);
-#else
-  if (h->P.protocol == PAXISIM_WPAXOS) return h->P.N == 9 ? occupancy<9, WPaxosProto>(h, blocks) : occupancy<0, WPaxosProto>(h, blocks);
-  if (h->P.protocol == PAXISIM_ABD)
-    return h->P.N == 3 ? occupancy<3, AbdProto>(h, blocks) : h->P.N == 5 ? occupancy<5, AbdProto>(h, blocks) : occupancy<0, AbdProto>(h, blocks);
-  switch (h->P.N) {
-    case 3: return occupancy<3, PaxosProto>(h, blocks);
-    case 5: return occupancy<5, PaxosProto>(h, blocks);
-    case 9: return occupancy<9, PaxosProto>(h, blocks);
-    default: return occupancy<0, PaxosProto>(h, blocks);
-  }
-#endif
-}
-
 static hipError_t launch_any(paxisim* h, uint32_t t0, uint32_t n) {
-#ifdef PXS_ONLY_PAXOS5   // tuning builds: the config-2 kernel only
-  if (h->P.protocol == PAXISIM_PAXOS && h->P.N == 5) return launch_steps<5, PaxosProto>(h, t0, n);
-  return hipErrorInvalidConfiguration;
-#else
-  if (h->P.protocol == PAXISIM_WPAXOS) {
-    switch (h->P.N) {
-      case 9: return launch_steps<9, WPaxosProto>(h, t0, n);
-      default: return launch_steps<0, WPaxosProto>(h, t0, n);
-    }
+  const int lds = (int)(h->P.G * h->P.lds_bytes);
+  if (h->lds_set != lds) {            // per handle, so per device
+    hipError_t e = h->ops.set_lds(lds);
+    if (e != hipSuccess) return e;
+    h->lds_set = lds;
   }
-  if (h->P.protocol == PAXISIM_ABD) {
-    switch (h->P.N) {
-      case 3: return launch_steps<3, AbdProto>(h, t0, n);
-      case 5: return launch_steps<5, AbdProto>(h, t0, n);
-      default: return launch_steps<0, AbdProto>(h, t0, n);
-    }
-  }
-  switch (h->P.N) {
-    case 3: return launch_steps<3, PaxosProto>(h, t0, n);
-    case 5: return launch_steps<5, PaxosProto>(h, t0, n);
-    case 9: return launch_steps<9, PaxosProto>(h, t0, n);
-    default: return launch_steps<0, PaxosProto>(h, t0, n);
-  }
-#endif
+  return h->ops.launch(h->P, h->stream, t0, n);
 }
 
 extern "C" int paxisim_step(paxisim* h, uint32_t nsteps) {
@@ -684,11 +661,18 @@ extern "C" int paxisim_step(paxisim* h, uint32_t nsteps) {
     const uint32_t n = nsteps < h->S ? nsteps : h->S;
     hipEvent_t a, b;
     HIPCHK(hipEventCreate(&a));
-    HIPCHK(hipEventCreate(&b));
-    HIPCHK(hipEventRecord(a, h->stream));
-    const hipError_t le = launch_any(h, h->t, n);
-    if (le != hipSuccess) return fail(PAXISIM_EDEVICE, "step launch: %s", hipGetErrorString(le));
-    HIPCHK(hipEventRecord(b, h->stream));
+    hipError_t e = hipEventCreate(&b);
+    if (e != hipSuccess) {
+      (void)hipEventDestroy(a);
+      return fail(PAXISIM_EDEVICE, "hipEventCreate: %s", hipGetErrorString(e));
+    }
+    if ((e = hipEventRecord(a, h->stream)) == hipSuccess && (e = launch_any(h, h->t, n)) == hipSuccess)
+      e = hipEventRecord(b, h->stream);
+    if (e != hipSuccess) {              // no leaked events on the error path
+      (void)hipEventDestroy(a);
+      (void)hipEventDestroy(b);
+      return fail(PAXISIM_EDEVICE, "step launch: %s", hipGetErrorString(e));
+    }
     h->evs.emplace_back(a, b);
     h->launches++;
     h->t += n;
@@ -719,6 +703,39 @@ extern "C" int paxisim_kernel_time(paxisim* h, double* ms, uint64_t* launches, i
     h->kernel_ms = 0;
     h->launches = 0;
   }
+  return 0;
+}
+
+extern "C" int paxisim_inject(paxisim* h, uint64_t cluster, uint32_t replica, uint32_t cid) {
+  if (!h) return fail(PAXISIM_EINVAL, "null handle");
+  if (cluster >= h->cfg.clusters || replica >= h->P.N || cid < 1 || cid > CMD_MASK)
+    return fail(PAXISIM_EINVAL, "bad inject (cluster %llu, replica %u, cid %u)", (unsigned long long)cluster,
+                replica, cid);
+  HIPCHK(hipSetDevice(h->cfg.device));
+  uint32_t st = 0;
+  inject_kernel<<<1, 64, 0, h->stream>>>(h->P, cluster, replica, h->t % h->P.D, cid, (uint32_t*)h->d_scratch);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(&st, h->d_scratch, sizeof st, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (st) return fail(PAXISIM_EINVAL, "client mailbox full");
+  return 0;
+}
+
+extern "C" int paxisim_read_log(paxisim* h, uint64_t cluster, uint32_t replica, uint32_t key, int32_t slot_lo,
+                                uint32_t n, paxisim_log_entry* out) {
+  if (!h || !out) return fail(PAXISIM_EINVAL, "null argument");
+  if (cluster >= h->cfg.clusters || replica >= h->P.N || key >= h->P.NK) return fail(PAXISIM_ERANGE, "bad entry");
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(h->cfg.device));
+  paxisim_log_entry* d = nullptr;
+  HIPCHK(hipMalloc(&d, n * sizeof(paxisim_log_entry)));
+  read_log_kernel<<<(n + 63) / 64, 64, 0, h->stream>>>(h->P, cluster, replica, key, slot_lo, n, d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d, n * sizeof(paxisim_log_entry), hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(PAXISIM_EDEVICE, "read_log: %s", hipGetErrorString(e));
+  for (uint32_t i = 0; i < n; i++) out[i].ballot = expand_ballot(h, (uint32_t)out[i].ballot);
   return 0;
 }
 
@@ -798,7 +815,7 @@ extern "C" int paxisim_check(paxisim* h, uint64_t* violations) {
 extern "C" int paxisim_occupancy(paxisim* h, int* blocks_per_cu, uint32_t* lds_bytes, uint32_t* staged) {
   if (!h || !blocks_per_cu) return fail(PAXISIM_EINVAL, "null argument");
   HIPCHK(hipSetDevice(h->cfg.device));
-  HIPCHK(occupancy_any(h, blocks_per_cu));
+  HIPCHK(h->ops.occupancy(h->P, blocks_per_cu));
   *blocks_per_cu *= (int)h->P.G;    // 64-cluster tiles resident per CU
   if (lds_bytes) *lds_bytes = h->P.lds_bytes;
   if (staged) *staged = h->P.J;
@@ -817,6 +834,7 @@ extern "C" int paxisim_history(paxisim* h, uint64_t cluster, uint32_t* buf, uint
   if (!h || !n_out) return fail(PAXISIM_EINVAL, "null argument");
   if (cluster >= h->cfg.clusters) return fail(PAXISIM_ERANGE, "cluster");
   HIPCHK(hipSetDevice(h->cfg.device));
+  HIPCHK(hipStreamSynchronize(h->stream));   // step kernels run on the non-blocking h->stream
   const Params& P = h->P;
   std::vector<uint32_t> len(P.N);
   for (uint32_t r = 0; r < P.N; r++)

@@ -23,7 +23,9 @@ constexpr uint32_t PMAX = 32;   // pending requests per replica (p.requests)
 constexpr uint32_t FMAX = 32;   // forwards table per replica (node.forwards)
 constexpr uint32_t CKI = 16;    // checkpoint interval (executed slots)
 constexpr uint32_t CKR = 8;     // checkpoints kept per replica
+constexpr uint32_t GMAX = 8;    // live entries below execute kept per instance
 constexpr uint32_t NO_ID = 0xFFu;
+constexpr uint32_t POL_NONE = 0xFFu;   // consecutive.last == "" (policy.go:50)
 constexpr uint32_t LANES = 64;
 constexpr uint32_t LDS_MAX = 160u * 1024u;
 constexpr uint32_t T_MAX = 1u << 28;   // slow_until is packed in 28 bits
@@ -93,6 +95,8 @@ struct Params {
   uint32_t npz[PAXISIM_MAX_ZONES], zmask[PAXISIM_MAX_ZONES];
   uint32_t zone_of[PAXISIM_MAX_N];   // 0-based zone of each replica
   uint32_t target[PAXISIM_MAX_WORKERS];
+  uint32_t start_step[PAXISIM_MAX_WORKERS];   // first request of worker w at this step
+  uint32_t late_workers;                      // mask of workers with start_step > 0
   Image img;
   uint32_t J, off_stage;   // LDS stage: J staged picks per replica at LDS byte off_stage ([r][J][64] x 16 B)
   uint32_t lds_bytes;      // LDS per cluster group (16-B multiple): the image + the stage
@@ -108,7 +112,7 @@ struct Params {
   uint32_t *link_drop, *link_slow;  // [dst][N][C]: drop_until; slow_until | delay << 28
   uint32_t* ck_e;        // [CKR][NI][C]
   uint64_t* ck_d;        // [CKR][NI][C]
-  uint4* gst;            // [NI][C] ghost-entry summary {slot lo, slot hi, ballot min, ballot max}
+  uint4* gst;            // [GMAX][NI][C] entries below execute {slot, ballot, until | commit << 31, 0}
   // WPaxos kpaxos instances, one 32-B state + a W-entry window + PMAX pending per
   // (blk, key, r, lane): {ballot, slot, execute, active|exists<<1|p1acks<<16,
   // npend, digest lo, digest hi, policy last|hits<<8}; entries {ballot, cmd|flags, acks, request}

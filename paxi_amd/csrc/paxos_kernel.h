@@ -112,30 +112,86 @@ __device__ __forceinline__ void raise_win(Rep<NT>& x, uint32_t f) {
   x.iflags |= f & (PAXISIM_F_WOVF | PAXISIM_F_GHOST);
 }
 
-// An entry Go would create or update below execute (a "ghost": update() or
-// HandleP2a on a slot already executed here) is not stored.  A ghost is inert
-// except to HandleP2b (paxos.go:270-310), which for m.Ballot >= e.ballot adopts
-// a higher ballot or, on m.Ballot == e.ballot owned by self, panics on the nil
-// quorum.  Per instance, a summary {slot lo, slot hi, ballot min, ballot max}
-// in HBM (rarely touched) keeps that observation detectable.
+// Entries below execute ("ghosts").  exec() deletes an
+// executed entry (paxos.go:366); update() (173-177), HandleP2a (254-258) and
+// HandleP3 (326) re-create one when a message for an executed slot arrives,
+// and Go keeps it.  Only HandleP2b (270-310) reads it: a P2b for the slot
+// adopts a higher ballot, or panics on the nil quorum when the ballot is this
+// replica's own and equals the entry's.  Such a P2b answers a P2a this replica
+// sent while the slot was >= execute, so it arrives within 2 + 2*max_delay
+// steps of the execution: a ghost lives that long after it is (re)created,
+// in a per-instance table in HBM {slot, ballot, until | commit << 31} touched
+// only on these paths.  iflags GHOST = the table may hold a live entry.
 template <int NT>
-__device__ __forceinline__ void ghost(const Params& P, Rep<NT>& x, int32_t s, uint32_t b) {
-  const size_t gi = (size_t)x.inst * P.C + x.c;
-  uint4 g = make_uint4(0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0u);
-  if (x.iflags & PAXISIM_F_GHOST) g = ldg(&P.gst[gi]);
-  raise_win(x, PAXISIM_F_GHOST);
-  g.x = min(g.x, (uint32_t)s);
-  g.y = max(g.y, (uint32_t)s);
-  g.z = min(g.z, b);
-  g.w = max(g.w, b);
-  P.gst[gi] = g;
+__device__ __forceinline__ size_t gidx(const Params& P, const Rep<NT>& x, uint32_t g) {
+  return ((size_t)g * P.NI + x.inst) * P.C + x.c;
 }
 template <int NT>
-__device__ __forceinline__ bool ghost_observed(const Params& P, const Rep<NT>& x, int32_t ms, uint32_t mb) {
-  if (!(x.iflags & PAXISIM_F_GHOST)) return false;
-  const uint4 g = ldg(&P.gst[(size_t)x.inst * P.C + x.c]);
-  if ((uint32_t)ms < g.x || (uint32_t)ms > g.y || mb < g.z) return false;
-  return mb > x.ballot || (bal_id(mb) == x.r && mb <= g.w);
+__device__ __forceinline__ uint32_t ghost_find(const Params& P, Rep<NT>& x, int32_t s, uint4& e) {
+  if (!(x.iflags & PAXISIM_F_GHOST)) return GMAX;
+  uint32_t live = 0, hit = GMAX;
+  for (uint32_t g = 0; g < GMAX; g++) {
+    const uint4 v = ldg(&P.gst[gidx<NT>(P, x, g)]);
+    const bool l = (v.z & 0x7FFFFFFFu) > x.t;
+    live |= l;
+    if (l && v.x == (uint32_t)s && hit == GMAX) { e = v; hit = g; }
+  }
+  if (!live) x.iflags &= ~PAXISIM_F_GHOST;               // every ghost has expired
+  return hit;
+}
+template <int NT>
+__device__ __forceinline__ uint32_t ghost_alloc(const Params& P, Rep<NT>& x) {
+  x.flags |= PAXISIM_F_GHOST;
+  for (uint32_t g = 0; g < GMAX; g++) {
+    const uint32_t until = ldg(&P.gst[gidx<NT>(P, x, g)]).z & 0x7FFFFFFFu;
+    if (!(x.iflags & PAXISIM_F_GHOST) || until <= x.t) {
+      x.iflags |= PAXISIM_F_GHOST;
+      return g;
+    }
+  }
+  x.flags |= PAXISIM_F_UNFAITHFUL;                       // cannot keep this ghost
+  return GMAX;
+}
+template <int NT>
+__device__ __forceinline__ uint32_t ghost_until(const Params& P, const Rep<NT>& x) {
+  return x.t + 3u + 2u * P.max_delay;
+}
+// update() / HandleP2a on a slot below execute: create, or raise an uncommitted ballot
+template <int NT>
+__device__ __forceinline__ void ghost(const Params& P, Rep<NT>& x, int32_t s, uint32_t b) {
+  uint4 e;
+  uint32_t g = ghost_find<NT>(P, x, s, e);
+  if (g < GMAX) {
+    if (!(e.z >> 31) && b > e.y) P.gst[gidx<NT>(P, x, g)] = make_uint4(e.x, b, e.z, 0u);
+    return;
+  }
+  if ((g = ghost_alloc<NT>(P, x)) < GMAX) P.gst[gidx<NT>(P, x, g)] = make_uint4((uint32_t)s, b, ghost_until<NT>(P, x), 0u);
+}
+// HandleP3 on a slot below execute: the entry exists and is committed (paxos.go:326-331)
+template <int NT>
+__device__ __forceinline__ void ghost_commit(const Params& P, Rep<NT>& x, int32_t s) {
+  uint4 e;
+  uint32_t g = ghost_find<NT>(P, x, s, e);
+  if (g < GMAX) {
+    P.gst[gidx<NT>(P, x, g)] = make_uint4(e.x, e.y, e.z | 0x80000000u, 0u);
+    return;
+  }
+  if ((g = ghost_alloc<NT>(P, x)) < GMAX)
+    P.gst[gidx<NT>(P, x, g)] = make_uint4((uint32_t)s, 0u, ghost_until<NT>(P, x) | 0x80000000u, 0u);
+}
+// HandleP2b (paxos.go:270-310) for a slot below execute
+template <int NT>
+__device__ __forceinline__ void ghost_p2b(const Params& P, Rep<NT>& x, int32_t ms, uint32_t mb) {
+  uint4 e;
+  if (ghost_find<NT>(P, x, ms, e) == GMAX || mb < e.y || (e.z >> 31)) return;
+  if (mb > x.ballot) {
+    x.ballot = mb;
+    x.active = 0;
+  }
+  if (bal_id(mb) == x.r && mb == e.y) {                  // nil quorum: Go panics
+    x.flags |= PAXISIM_F_POISON;
+    x.stop = true;
+  }
 }
 
 template <int NT>
@@ -339,8 +395,8 @@ template <int NT>
 __device__ __forceinline__ void paxos_handle_p2b(const Params& P, Rep<NT>& x, uint32_t src, uint32_t mb,
                                                  int32_t ms) {                // paxos.go:270-310
   if (!in_window<NT>(P, x, ms)) {
-    if (ms < x.execute ? ghost_observed<NT>(P, x, ms, mb) : (x.iflags & PAXISIM_F_WOVF) != 0)
-      x.flags |= PAXISIM_F_UNFAITHFUL;
+    if (ms < x.execute) ghost_p2b<NT>(P, x, ms, mb);
+    else if (x.iflags & PAXISIM_F_WOVF) x.flags |= PAXISIM_F_UNFAITHFUL;
     return;
   }
   const uint32_t i = eidx<NT>(P, x, ms);
@@ -401,7 +457,7 @@ __device__ __forceinline__ void paxos_handle_p3(const Params& P, Rep<NT>& x, uin
       return;
     }
   } else if (ms < x.execute) {
-    raise_win(x, PAXISIM_F_GHOST);
+    ghost_commit<NT>(P, x, ms);
   } else {
     raise_win(x, PAXISIM_F_WOVF);
   }

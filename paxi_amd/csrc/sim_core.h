@@ -295,6 +295,28 @@ __device__ __forceinline__ void client_reply(const Params& P, Rep<NT>& x, uint32
   }
 }
 
+// A worker whose first request is due at this step sends it to its target
+// now (paxisim_workload.start_step), behind the requests already queued there.
+template <int NT>
+__device__ __forceinline__ void client_start(const Params& P, Rep<NT>& x) {
+  for (uint32_t m = P.late_workers; m; m &= m - 1u) {   // scalar loop: the mask is uniform
+    const uint32_t w = (uint32_t)__builtin_ctz(m);
+    if (P.start_step[w] != x.t || P.target[w] != x.r) continue;
+    const uint32_t wi = (w << 6) | x.lane;
+    x.l_wcur[wi] = 1u + w;
+    x.l_wiss[wi] = 1u;
+    const uint32_t box = (x.b0 * nrep<NT>(P) + x.r) * P.NS + nrep<NT>(P);
+    uint8_t* cp = &x.l_cnt[(box << 6) | x.lane];
+    const uint32_t k = *cp;
+    if (k >= P.M) {
+      x.flags |= PAXISIM_F_MBOX_OVF | PAXISIM_F_UNFAITHFUL;
+      continue;
+    }
+    x.rec[((box * P.M + k) << 6) | x.lane] = make_uint4(PAXISIM_MSG_REQUEST, 0u, 0u, 1u + w);
+    *cp = (uint8_t)(k + 1u);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Random fault process: per idle outgoing link, one draw may open a drop and
 // / or a slow window.
@@ -363,6 +385,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
   x.stop = false;
   x.im = 0;
   x.hs = step_key(x.kc, x.t);
+  if (P.late_workers) client_start<NT>(P, x);
   {
     uint32_t du[Rep<NT>::NL], su[Rep<NT>::NL];
 #pragma unroll
@@ -586,7 +609,7 @@ template <int NT> constexpr int min_waves() { return NT == 0 ? 4 : 3; }
 // Instances that carry the LDS-staged merge loop.  Staging only pays where a
 // workgroup runs alone on its CU and has LDS to spare (9 replicas, ABD's 3/5);
 // elsewhere the second copy of the loop costs registers the packed cluster
-// groups need.  paxisim.hip mirrors this (stage_built_host) and sets J = 0.
+// groups need.  StepOps::staged exports it (step_ops.h); paxisim.hip sets J = 0 without it.
 template <int NT, class Proto> constexpr bool stage_built() {
   return Proto::kind == PAXISIM_ABD ? NT != 0 : NT == 9;
 }

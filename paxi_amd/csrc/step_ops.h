@@ -1,0 +1,60 @@
+// step_ops.h — host-side launchers of the step kernel instances.
+//
+// Each protocol's sim_steps<N, Proto> instances are compiled in their own
+// translation unit (k_*.hip) so the library builds in parallel; paxisim.hip
+// reaches them only through this table of function pointers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "paxisim_dev.h"
+
+namespace pxs {
+
+struct StepOps {
+  // launch grid = P.C / (64 * P.G) workgroups of P.G*N waves, P.G * P.lds_bytes of LDS
+  hipError_t (*launch)(const Params& P, hipStream_t s, uint32_t t0, uint32_t n);
+  // set the dynamic-LDS ceiling of the instance on the current device
+  hipError_t (*set_lds)(int bytes);
+  hipError_t (*occupancy)(const Params& P, int* blocks);
+  hipError_t (*attrs)(int* vgprs, int* max_threads);
+  bool staged;   // the instance carries the LDS-staged merge loop (sim_core.h stage_built)
+};
+
+// defined in k_paxos*.hip, k_abd.hip, k_wpaxos.hip; nullptr launch = not built
+StepOps paxos_step_ops(uint32_t N);
+StepOps abd_step_ops(uint32_t N);
+StepOps wpaxos_step_ops(uint32_t N);
+
+#ifdef PXS_STEP_INSTANCE   // included by a kernel translation unit
+template <int NT, class Proto>
+struct StepInstance {
+  static hipError_t launch(const Params& P, hipStream_t s, uint32_t t0, uint32_t n) {
+    const unsigned grid = (unsigned)(P.C / (LANES * P.G));
+    sim_steps<NT, Proto><<<grid, P.G * P.N * LANES, (size_t)P.G * P.lds_bytes, s>>>(P, t0, n);
+    return hipGetLastError();
+  }
+  // The ceiling is set to what the launch uses, not to the CU's 160 KB: the
+  // runtime sizes every workgroup's LDS allocation by it, and a 160 KB ceiling
+  // would hold each CU to one resident workgroup.
+  static hipError_t set_lds(int bytes) {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&sim_steps<NT, Proto>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  }
+  static hipError_t occupancy(const Params& P, int* blocks) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, reinterpret_cast<const void*>(&sim_steps<NT, Proto>),
+                                                        (int)(P.G * P.N * LANES), (size_t)P.G * P.lds_bytes);
+  }
+  static hipError_t attrs(int* v, int* maxthr) {
+    hipFuncAttributes a;
+    hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&sim_steps<NT, Proto>));
+    if (e == hipSuccess) {
+      *v = a.numRegs;
+      *maxthr = a.maxThreadsPerBlock;
+    }
+    return e;
+  }
+  static StepOps ops() { return StepOps{&launch, &set_lds, &occupancy, &attrs, stage_built<NT, Proto>()}; }
+};
+#endif
+
+}  // namespace pxs

@@ -25,8 +25,6 @@
 
 namespace pxs {
 
-constexpr uint32_t POL_NONE = 0xFFu;   // consecutive.last == "" (policy.go:50)
-
 // The majority / ema policies run only on a leader's request path; built out
 // of line (PXS_POLICY_NOINLINE=1) they stay out of the merge loop's registers.
 #if defined(PXS_POLICY_NOINLINE) && PXS_POLICY_NOINLINE

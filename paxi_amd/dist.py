@@ -10,8 +10,9 @@ over xGMI on MI355X; tests use "gloo" on the CPU.
 import os
 
 # order of the per-rank counter vector that gets all-reduced
+FLAG_NAMES = ("WOVF", "GHOST", "MBOX_OVF", "PEND_OVF", "UNFAITHFUL", "POISON", "BALLOT_OVF", "HIST_OVF")
 COUNTERS = ("delivered_total", "commits", "replies", "dropped", "client_requests", "alg_bytes",
-            "violations", "unfaithful", "poisoned")
+            "violations") + tuple("flag_" + n for n in FLAG_NAMES)
 
 
 def env_rank():
@@ -41,6 +42,8 @@ def reduce_counters(values, elapsed, device=None, group=None):
 def stats_counters(delta, alg_bytes=0, violations=0, flagged=None):
     """Counter dict from a stats delta (bench.stats_delta) and scan results."""
     flagged = flagged or [0] * 8
-    return {"delivered_total": delta["delivered_total"], "commits": delta["commits"], "replies": delta["replies"],
-            "dropped": delta["dropped"], "client_requests": delta["client_requests"], "alg_bytes": alg_bytes,
-            "violations": violations, "unfaithful": flagged[4], "poisoned": flagged[5]}
+    d = {"delivered_total": delta["delivered_total"], "commits": delta["commits"], "replies": delta["replies"],
+         "dropped": delta["dropped"], "client_requests": delta["client_requests"], "alg_bytes": alg_bytes,
+         "violations": violations}
+    d.update({"flag_" + n: flagged[i] for i, n in enumerate(FLAG_NAMES)})
+    return d

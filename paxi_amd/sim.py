@@ -57,7 +57,7 @@ def load_library():
 EXPORTED = ["paxisim_abi_version", "paxisim_last_error", "paxisim_create", "paxisim_destroy",
             "paxisim_fault_add", "paxisim_step", "paxisim_sync", "paxisim_stats_get",
             "paxisim_read_state", "paxisim_read_instances", "paxisim_check", "paxisim_kernel_time", "paxisim_device_bytes",
-            "paxisim_linearizable", "paxisim_history", "paxisim_occupancy"]
+            "paxisim_linearizable", "paxisim_history", "paxisim_occupancy", "paxisim_inject", "paxisim_read_log"]
 
 
 def _check(rc):
@@ -109,6 +109,16 @@ class Simulation:
         v = C.c_uint64()
         _check(load_library().paxisim_check(self.h, C.byref(v)))
         return v.value
+
+    def inject(self, cluster, replica, cid):
+        """A client request for command `cid` at `replica` in the next step (http.go:99)."""
+        _check(load_library().paxisim_inject(self.h, cluster, replica, cid))
+
+    def read_log(self, cluster, replica, slot_lo, n, key=0):
+        """paxos.go entries of slots [slot_lo, slot_lo+n) of one instance (paxisim_read_log)."""
+        arr = (abi.LogEntry * max(1, n))()
+        _check(load_library().paxisim_read_log(self.h, cluster, replica, key, slot_lo, n, arr))
+        return list(arr[:n])
 
     def linearizable(self):
         """History.Linearizable (history.go:55-71): (anomalies, ops checked, partitions skipped)."""

@@ -83,6 +83,14 @@ class OracleSim:
         _check(lib().oracle_check(self.h, C.byref(v)))
         return v.value
 
+    def inject(self, cluster, replica, cid):
+        _check(lib().oracle_inject(self.h, cluster, replica, cid))
+
+    def read_log(self, cluster, replica, slot_lo, n, key=0):
+        arr = (abi.LogEntry * max(1, n))()
+        _check(lib().oracle_read_log(self.h, cluster, replica, key, slot_lo, n, arr))
+        return list(arr[:n])
+
     def exec_log(self, cluster, replica, key=0):
         rk = replica | (key << 16)
         n = C.c_uint32()

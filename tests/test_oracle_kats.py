@@ -92,3 +92,15 @@ def test_config1_independent_of_seed():
     a.step(3010)
     b.step(3010)
     assert a.stats().delivered_total == b.stats().delivered_total == k["delivered_total"]
+
+
+def test_inject_validates_arguments():
+    sim, _ = _config1()
+    with pytest.raises(RuntimeError):
+        sim.inject(0, 3, 5)          # replica out of range
+    with pytest.raises(RuntimeError):
+        sim.inject(0, 0, 0)          # cid 0 is nil
+    for k in range(16):
+        sim.inject(0, 1, 100 + k)
+    with pytest.raises(RuntimeError, match="mailbox full"):
+        sim.inject(0, 1, 200)        # 1 worker request + 16 injected > mbox_cap 16

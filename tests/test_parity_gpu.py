@@ -160,3 +160,39 @@ def test_window32_n5():
     fp = abi.make_fault_process(drop_ppm=3000, drop_len=25, slow_ppm=3000, slow_len=25, slow_min=1, slow_max=4)
     g, o = run_both(cfg, wl, fp, steps=300)
     assert_same(g, o, "W=32")
+
+
+def test_late_workers_crash_failover():
+    """Config-4 shape: clients turn from the crashed leader 1.1 to 2.1 (start_step), FGrid fz=1."""
+    cfg = abi.make_config(npz=[3, 3, 3], clusters=130, seed=8, q1=abi.Q_FGRID_Q1, q2=abi.Q_FGRID_Q2, fz=1,
+                          ephemeral_leader=1, mbox_cap=24, max_delay=0)
+    wl = abi.make_workload(outstanding=8, target=[0, 0, 0, 0, 3, 3, 3, 3], start_step=[0, 0, 0, 0, 90, 90, 90, 90])
+    g, o = run_both(cfg, wl, None, [abi.make_fault(abi.FAULT_CRASH, 0, step_from=90)], chunks=[60, 60, 120])
+    st = assert_same(g, o, "failover")
+    s = g.read_state()
+    assert st["discarded"] > 0 and all(s[c * 9 + 3].active == 1 for c in range(130))
+
+
+def test_inject_and_read_log():
+    """Injected client requests (http.go:99) and the log windows, entry by entry."""
+    cfg = abi.make_config(npz=[5], clusters=70, seed=13, window=16, mbox_cap=16, max_delay=3, ephemeral_leader=1)
+    wl = abi.make_workload(outstanding=2, target=0, max_requests=40)
+    fp = abi.make_fault_process(drop_ppm=20000, drop_len=5, slow_ppm=20000, slow_len=5, slow_min=1, slow_max=3)
+    g = _sim()(cfg, wl, fp)
+    o = ol.OracleSim(cfg, wl, fp)
+    cid = 1 << 20
+    for step in range(12):
+        for c in range(0, 70, 3):
+            r = (c + step) % 5
+            g.inject(c, r, cid)
+            o.inject(c, r, cid)
+            cid += 1
+        g.step(9)
+        o.step(9)
+    assert_same(g, o, "inject")
+    for c in range(0, 70, 7):
+        for r in range(5):
+            e = min(x.execute for x in o.read_state(c, 1))
+            a = [x.as_tuple() for x in g.read_log(c, r, e - 2, 20)]
+            b = [x.as_tuple() for x in o.read_log(c, r, e - 2, 20)]
+            assert a == b, f"cluster {c} replica {r}"
