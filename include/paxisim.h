@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PAXISIM_ABI_VERSION 6
+#define PAXISIM_ABI_VERSION 7
 
 #define PAXISIM_MAX_N        16  /* replicas per cluster (ack masks are u16) */
 #define PAXISIM_MAX_ZONES    16
@@ -326,6 +326,13 @@ int  paxisim_linearizable(paxisim* h, uint64_t* anomalies, uint64_t* ops, uint64
  * is_write, value, start step, end step}; replicas in index order, each in
  * completion order (the canonical history order). */
 int  paxisim_history(paxisim* h, uint64_t cluster, uint32_t* buf, uint32_t cap_ops, uint32_t* n_out);
+
+/* History.ReadFile (history.go:115-178) into the device: replace the recorded
+ * operations of one replica of a local cluster with n ops in the format of
+ * paxisim_history (5 words each; n <= config.history), so that
+ * paxisim_linearizable checks an imported history (e.g. one written by the
+ * reference's client) on the GPU.  ABD handles only. */
+int  paxisim_history_load(paxisim* h, uint64_t cluster, uint32_t replica, const uint32_t* ops, uint32_t n);
 
 /* 64-cluster tiles of the step kernel resident per CU (hipOccupancy x tiles
  * per workgroup), LDS per tile, and messages staged into LDS per

@@ -1763,3 +1763,15 @@ int oracle_history(oracle_sim* s, uint64_t cl, uint32_t* buf, uint32_t cap_ops, 
   *n_out = n;
   return 0;
 }
+
+/* History.ReadFile (history.go:115-178): replace replica r's recorded ops of
+ * one cluster, 5 words per op as oracle_history returns them. */
+int oracle_history_load(oracle_sim* s, uint64_t cl, uint32_t r, const uint32_t* ops, uint32_t n) {
+  uint32_t j;
+  if (!s || (n && !ops) || cl >= s->C || r >= s->N) return fail(PAXISIM_EINVAL, "bad argument");
+  if (s->cfg.protocol != PAXISIM_ABD) return fail(PAXISIM_EUNSUPP, "op history is kept by ABD only");
+  if (n > s->cfg.history) return fail(PAXISIM_EINVAL, "%u ops exceed history capacity %u", n, s->cfg.history);
+  for (j = 0; j < n; j++) memcpy(&s->cl[cl].rep[r].hist[j], ops + 5 * (size_t)j, sizeof(hist_t));
+  s->cl[cl].rep[r].nh = n;
+  return 0;
+}

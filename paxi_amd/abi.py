@@ -6,7 +6,7 @@ structs, so the two speak exactly the same ABI.
 """
 import ctypes as C
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 MAX_N = 16
 MAX_ZONES = 16
 MAX_WORKERS = 32
@@ -192,6 +192,7 @@ def declare(lib, prefix):
         "check": (C.c_int, [h, P(C.c_uint64)]),
         "inject": (C.c_int, [h, C.c_uint64, C.c_uint32, C.c_uint32]),
         "read_log": (C.c_int, [h, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int32, C.c_uint32, P(LogEntry)]),
+        "history_load": (C.c_int, [h, C.c_uint64, C.c_uint32, P(C.c_uint32), C.c_uint32]),
         "last_error": (C.c_char_p, []),
     }
     for name, (res, args) in spec.items():

@@ -859,6 +859,28 @@ extern "C" int paxisim_history(paxisim* h, uint64_t cluster, uint32_t* buf, uint
   return 0;
 }
 
+// History.ReadFile (history.go:115-178) into the device history of one replica.
+extern "C" int paxisim_history_load(paxisim* h, uint64_t cluster, uint32_t replica, const uint32_t* ops, uint32_t n) {
+  if (!h || (n && !ops)) return fail(PAXISIM_EINVAL, "null argument");
+  if (cluster >= h->cfg.clusters || replica >= h->P.N) return fail(PAXISIM_ERANGE, "bad replica");
+  if (h->P.protocol != PAXISIM_ABD) return fail(PAXISIM_EUNSUPP, "op history is kept by ABD only");
+  if (n > h->P.H) return fail(PAXISIM_EINVAL, "%u ops exceed history capacity %u", n, h->P.H);
+  HIPCHK(hipSetDevice(h->cfg.device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  const Params& P = h->P;
+  std::vector<uint4> tmp(n ? n : 1);
+  for (uint32_t j = 0; j < n; j++) {
+    const uint32_t* o = ops + 5 * (size_t)j;
+    if (o[0] > 0x7FFFFFFFu || o[1] > 1u) return fail(PAXISIM_EINVAL, "op %u: bad key or is_write", j);
+    tmp[j] = make_uint4(o[0] | (o[1] << 31), o[2], o[3], o[4]);
+  }
+  if (n)
+    HIPCHK(hipMemcpy(&P.hist[((size_t)replica * P.C + cluster) * P.H], tmp.data(), n * sizeof(uint4),
+                     hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(&P.execute[rc_host(P, replica, cluster)], &n, 4, hipMemcpyHostToDevice));
+  return 0;
+}
+
 extern "C" int paxisim_linearizable(paxisim* h, uint64_t* anomalies, uint64_t* ops, uint64_t* skipped) {
   if (!h) return fail(PAXISIM_EINVAL, "null handle");
   if (h->P.protocol != PAXISIM_ABD || h->P.H == 0)

@@ -57,7 +57,8 @@ def load_library():
 EXPORTED = ["paxisim_abi_version", "paxisim_last_error", "paxisim_create", "paxisim_destroy",
             "paxisim_fault_add", "paxisim_step", "paxisim_sync", "paxisim_stats_get",
             "paxisim_read_state", "paxisim_read_instances", "paxisim_check", "paxisim_kernel_time", "paxisim_device_bytes",
-            "paxisim_linearizable", "paxisim_history", "paxisim_occupancy", "paxisim_inject", "paxisim_read_log"]
+            "paxisim_linearizable", "paxisim_history", "paxisim_occupancy", "paxisim_inject", "paxisim_read_log",
+            "paxisim_history_load"]
 
 
 def _check(rc):
@@ -132,6 +133,13 @@ class Simulation:
         buf = (C.c_uint32 * max(1, 5 * n.value))()
         _check(load_library().paxisim_history(self.h, cluster, buf, n.value, C.byref(n)))
         return [tuple(buf[5 * i: 5 * i + 5]) for i in range(n.value)]
+
+    def history_load(self, cluster, replica, ops):
+        """History.ReadFile into the device (paxisim_history_load): ops are
+        (key, is_write, value, start, end) tuples."""
+        flat = [int(v) for o in ops for v in o]
+        buf = (C.c_uint32 * max(1, len(flat)))(*flat)
+        _check(load_library().paxisim_history_load(self.h, cluster, replica, buf, len(ops)))
 
     def kernel_time(self, reset=False):
         ms, n = C.c_double(), C.c_uint64()

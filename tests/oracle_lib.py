@@ -111,6 +111,11 @@ class OracleSim:
         _check(lib().oracle_history(self.h, cluster, buf, n.value, C.byref(n)))
         return [tuple(buf[5 * i: 5 * i + 5]) for i in range(n.value)]
 
+    def history_load(self, cluster, replica, ops):
+        flat = [int(v) for o in ops for v in o]
+        buf = (C.c_uint32 * max(1, len(flat)))(*flat)
+        _check(lib().oracle_history_load(self.h, cluster, replica, buf, len(ops)))
+
     def close(self):
         if self.h:
             lib().oracle_destroy(self.h)

@@ -82,3 +82,13 @@ def test_history_export_from_device(tmp_path):
         b.write_file(str(tmp_path / f"o{c}"))
         assert (tmp_path / f"g{c}.csv").read_text() == (tmp_path / f"o{c}.csv").read_text()
         assert len(a.operations) > 10
+
+
+def test_history_straight_after_step():
+    """paxisim_history right after paxisim_step, with no other read between:
+    the read must wait for the step kernels on the handle's stream."""
+    g, o = make(4096, keys=4, history=64)
+    g.step(120)
+    o.step(120)
+    for c in (0, 2047, 4095):
+        assert g.history(c) == o.history(c)
