@@ -339,6 +339,13 @@ int  paxisim_history_load(paxisim* h, uint64_t cluster, uint32_t replica, const 
  * replica-step (any pointer but the first may be NULL). */
 int  paxisim_occupancy(paxisim* h, int* blocks_per_cu, uint32_t* lds_bytes, uint32_t* staged);
 
+/* Clusters still stepped: a Paxos cluster whose mailboxes are all empty is at
+ * a fixed point (no timers, no retries: paxos/paxos.go) and is frozen and
+ * packed behind the active ones; an injected request wakes it.  Results are
+ * identical either way; this reports how many clusters the
+ * step kernels still visit. */
+int  paxisim_active_clusters(paxisim* h, uint64_t* active);
+
 /* Bytes of device memory held by the handle. */
 int  paxisim_device_bytes(paxisim* h, uint64_t* bytes);
 

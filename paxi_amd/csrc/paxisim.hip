@@ -15,6 +15,7 @@
 
 #include "lin_kernel.h"
 #include "paxisim_dev.h"
+#include "sim_core.h"
 #include "step_ops.h"
 
 using namespace pxs;
@@ -53,6 +54,13 @@ struct paxisim {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
   double kernel_ms = 0;
   uint64_t launches = 0;
+  // live-cluster compaction
+  uint32_t* d_cmp = nullptr;       // [0] bound, [1] lnew, [2] npairs, [3] live, [4] live before lnew, then block sums
+  uint32_t* d_pairs = nullptr;     // [2][C/2+64]: dead slots below lnew, live slots above it
+  uint32_t cmp_every = 50;         // steps between compactions
+  uint32_t last_cmp = 0;
+  uint32_t late_until = 0;         // no compaction before every late worker has started
+  uint32_t bound_host = 0;         // last bound read back (diagnostics)
 };
 
 static inline size_t rc_host(const Params& P, uint32_t r, uint64_t c) { return (size_t)r * P.C + c; }
@@ -76,6 +84,8 @@ __global__ void init_kernel(Params P) {
   const uint32_t blk = (uint32_t)(c / LANES), lane = (uint32_t)(c % LANES);
   uint8_t* img = P.image + (size_t)blk * P.img.bytes;
   P.kc[c] = cluster_key(P.seed, P.cluster_base + c);
+  P.slot_of[c] = (uint32_t)c;
+  P.cl_of[c] = (uint32_t)c;
   reinterpret_cast<uint32_t*>(img + P.img.off_poison)[lane] = 0xFFFFFFFFu;
   if (P.protocol == PAXISIM_PAXOS)
     for (uint32_t r = 0; r < P.N; r++) P.slot[rc(P, r, c)] = 0xFFFFFFFFu;   // slot: -1 (paxos.go:45)
@@ -131,7 +141,7 @@ __global__ void stats_kernel(Params P, uint64_t* out) {
 __global__ void gather_kernel(Params P, uint64_t lo, uint64_t n, paxisim_replica_state* out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * P.N) return;
-  const uint64_t c = lo + i / P.N;
+  const uint64_t c = slot_of(P, lo + i / P.N);
   const uint32_t r = (uint32_t)(i % P.N);
   const size_t j = rc(P, r, c);
   paxisim_replica_state s;
@@ -203,7 +213,7 @@ __global__ void gather_kernel(Params P, uint64_t lo, uint64_t n, paxisim_replica
 __global__ void gather_inst_kernel(Params P, uint64_t lo, uint64_t n, paxisim_instance_state* out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * P.NI) return;
-  const uint64_t c = lo + i / P.NI;
+  const uint64_t c = slot_of(P, lo + i / P.NI);
   const uint32_t r = (uint32_t)((i / P.NK) % P.N), k = (uint32_t)(i % P.NK);
   paxisim_instance_state s;
   memset(&s, 0, sizeof s);
@@ -290,8 +300,9 @@ __global__ void check_kernel(Params P, uint64_t* out) {
 }
 
 // paxisim_inject: one client request record into (bucket b, dst r, src client)
-__global__ void inject_kernel(Params P, uint64_t c, uint32_t r, uint32_t b, uint32_t cid, uint32_t* status) {
+__global__ void inject_kernel(Params P, uint64_t cl, uint32_t r, uint32_t b, uint32_t cid, uint32_t* status) {
   if (threadIdx.x != 0) return;
+  const uint64_t c = slot_of(P, cl);
   const uint32_t blk = (uint32_t)(c / LANES), lane = (uint32_t)(c % LANES);
   uint8_t* cnt = P.image + (size_t)blk * P.img.bytes + P.img.off_cnt;
   const uint32_t box = (b * P.N + r) * P.NS + P.N;
@@ -306,10 +317,11 @@ __global__ void inject_kernel(Params P, uint64_t c, uint32_t r, uint32_t b, uint
 }
 
 // paxisim_read_log: one thread per slot of one instance's window
-__global__ void read_log_kernel(Params P, uint64_t c, uint32_t r, uint32_t key, int32_t lo, uint32_t n,
+__global__ void read_log_kernel(Params P, uint64_t cl, uint32_t r, uint32_t key, int32_t lo, uint32_t n,
                                 paxisim_log_entry* out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  const uint64_t c = slot_of(P, cl);
   const uint32_t blk = (uint32_t)(c / LANES), lane = (uint32_t)(c % LANES);
   const int32_t s = lo + (int32_t)i;
   paxisim_log_entry o;
@@ -345,6 +357,195 @@ __global__ void read_log_kernel(Params P, uint64_t c, uint32_t r, uint32_t key, 
     }
   }
   out[i] = o;
+}
+
+
+// ---------------------------------------------------------------------------
+// Live-cluster compaction.  A Paxos cluster whose mailboxes
+// are empty at the end of a launch is at a fixed point: Paxi has no timers or
+// retries, so nothing in it changes again unless a request is injected.  Its
+// only evolving state is the random fault process of its links, which no
+// handler can observe while no message moves.  Every cmp_every steps the
+// slots [0, bound) are partitioned so that live clusters fill whole 64-cluster
+// tiles at the front: the k-th quiescent slot below lnew swaps all its state
+// with the k-th live slot above it, and slots [lnew, bound) freeze (frz =
+// the step they stopped at).  Workgroups past the bound exit at once, so
+// launches stop paying for lanes whose clusters have died.  A request
+// injected into a frozen cluster wakes its tile: the link fault process is
+// replayed over the frozen steps, so the trajectory is exactly the one the
+// oracle computes without any of this.
+// ---------------------------------------------------------------------------
+constexpr uint32_t CB = 1024;                    // slots per counting block
+enum { CM_BOUND = 0, CM_LNEW, CM_NPAIRS, CM_LIVE, CM_LBL, CM_SUMS = 8 };
+
+template <typename T>
+__device__ __forceinline__ void swap_rows(T* a, size_t rows, size_t C, uint64_t p, uint64_t q, uint32_t j) {
+  for (size_t k = j; k < rows; k += LANES) {
+    const T v = a[k * C + p];
+    a[k * C + p] = a[k * C + q];
+    a[k * C + q] = v;
+  }
+}
+// lane-fastest per-block regions: element (row, lane) of block b at base + b*bstride + row*64 + lane
+template <typename T>
+__device__ __forceinline__ void swap_lanes(T* base, size_t bstride, size_t rows, uint64_t p, uint64_t q, uint32_t j) {
+  T* bp = base + (p / LANES) * bstride + (p % LANES);
+  T* bq = base + (q / LANES) * bstride + (q % LANES);
+  for (size_t k = j; k < rows; k += LANES) {
+    const T v = bp[k * LANES];
+    bp[k * LANES] = bq[k * LANES];
+    bq[k * LANES] = v;
+  }
+}
+
+// Swap every per-slot datum of the Paxos step kernel between slots p and q
+// (one wave per pair, lane j takes every 64th element).
+__device__ void swap_slots(const Params& P, uint64_t p, uint64_t q, uint32_t j) {
+  const size_t C = P.C, N = P.N;
+  swap_rows(P.ballot, 7 * N, C, p, q, j);        // ballot slot execute meta flags npend nfwd
+  swap_rows(P.digest, N, C, p, q, j);
+  swap_rows(P.kc, 1, C, p, q, j);
+  swap_rows(P.pend, (size_t)PMAX * P.NI, C, p, q, j);
+  swap_rows(P.fwd, (size_t)FMAX * N, C, p, q, j);
+  swap_rows(P.link_drop, 2 * N * N, C, p, q, j);   // link_drop then link_slow
+  swap_rows(P.ck_e, (size_t)CKR * P.NI, C, p, q, j);
+  swap_rows(P.ck_d, (size_t)CKR * P.NI, C, p, q, j);
+  swap_rows(P.gst, (size_t)GMAX * P.NI, C, p, q, j);
+  swap_rows(P.stats, (size_t)NSTAT * N, C, p, q, j);
+  swap_rows(P.frz, 1, C, p, q, j);
+  swap_rows(P.qf, 1, C, p, q, j);
+  swap_lanes(P.reqx, (size_t)N * P.W * LANES, (size_t)N * P.W, p, q, j);
+  // LDS image: u32 rows (log window a/b/c, worker tables, poison), then u8 mailbox counts
+  swap_lanes(reinterpret_cast<uint32_t*>(P.image), P.img.bytes / 4u, P.img.off_cnt / (LANES * 4u), p, q, j);
+  {
+    uint8_t* cp = P.image + (p / LANES) * (size_t)P.img.bytes + P.img.off_cnt + (p % LANES);
+    uint8_t* cq = P.image + (q / LANES) * (size_t)P.img.bytes + P.img.off_cnt + (q % LANES);
+    uint4* rp = P.rec + (p / LANES) * (size_t)P.rec_per_block + (p % LANES);
+    uint4* rq = P.rec + (q / LANES) * (size_t)P.rec_per_block + (q % LANES);
+    const uint32_t nbox = P.D * P.N * P.NS;
+    for (uint32_t b = j; b < nbox; b += LANES) {           // records in flight, then their counts
+      const uint32_t kp = cp[b * LANES], kq = cq[b * LANES];
+      const uint32_t kn = kp > kq ? kp : kq;
+      for (uint32_t k = 0; k < kn; k++) {
+        const size_t o = (size_t)(b * P.M + k) * LANES;
+        const uint4 v = rp[o];
+        rp[o] = rq[o];
+        rq[o] = v;
+      }
+      cp[b * LANES] = (uint8_t)kq;
+      cq[b * LANES] = (uint8_t)kp;
+    }
+  }
+  if (j == 0) {
+    const uint32_t a = P.cl_of[p], b = P.cl_of[q];
+    P.cl_of[p] = b;
+    P.cl_of[q] = a;
+    P.slot_of[b] = (uint32_t)p;
+    P.slot_of[a] = (uint32_t)q;
+  }
+}
+
+__global__ void cmp_count(Params P, uint32_t* cm) {
+  const uint64_t s = (uint64_t)blockIdx.x * CB + threadIdx.x;
+  const int live = s < cm[CM_BOUND] && !P.qf[s];
+  const int n = __syncthreads_count(live);
+  if (threadIdx.x == 0) cm[CM_SUMS + blockIdx.x] = (uint32_t)n;
+}
+
+// one workgroup of CB threads: exclusive scan of the block counts, then the
+// new bound and the number of pairs to swap
+__global__ void cmp_scan(Params P, uint32_t* cm, uint32_t nb) {
+  __shared__ uint32_t sh[CB];
+  __shared__ uint32_t carry;
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < nb; base += CB) {
+    const uint32_t v = base + tid < nb ? cm[CM_SUMS + base + tid] : 0u;
+    sh[tid] = v;
+    __syncthreads();
+    for (uint32_t off = 1; off < CB; off <<= 1) {
+      const uint32_t t = tid >= off ? sh[tid - off] : 0u;
+      __syncthreads();
+      sh[tid] += t;
+      __syncthreads();
+    }
+    if (base + tid < nb) cm[CM_SUMS + base + tid] = carry + sh[tid] - v;
+    __syncthreads();
+    if (tid == 0) carry += sh[CB - 1];
+    __syncthreads();
+  }
+  const uint32_t live = carry, bound = cm[CM_BOUND];
+  uint32_t lnew = (live + LANES - 1u) / LANES * LANES;
+  if (lnew > bound) lnew = bound;
+  const uint32_t b = lnew / CB;
+  const uint64_t s = (uint64_t)b * CB + tid;
+  const int cnt = __syncthreads_count(s < lnew && !P.qf[s]);
+  const uint32_t lbl = (b < nb ? cm[CM_SUMS + b] : live) + (uint32_t)cnt;   // live slots below lnew
+  if (tid == 0) {
+    cm[CM_LNEW] = lnew;
+    cm[CM_LIVE] = live;
+    cm[CM_LBL] = lbl;
+    cm[CM_NPAIRS] = live - lbl;
+  }
+}
+
+__global__ void cmp_index(Params P, uint32_t* cm, uint32_t* lo, uint32_t* hi) {
+  __shared__ uint32_t wsum[CB / LANES];
+  const uint64_t s = (uint64_t)blockIdx.x * CB + threadIdx.x;
+  const uint32_t bound = cm[CM_BOUND], lnew = cm[CM_LNEW], lbl = cm[CM_LBL], np = cm[CM_NPAIRS];
+  const bool live = s < bound && !P.qf[s];
+  const uint64_t m = __ballot(live);
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint32_t inw = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+  if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
+  __syncthreads();
+  uint32_t off = 0;
+  for (uint32_t k = 0; k < w; k++) off += wsum[k];
+  const uint32_t before = cm[CM_SUMS + blockIdx.x] + off + inw;     // live slots in [0, s)
+  if (s >= bound) return;
+  if (!live && s < lnew) {
+    const uint32_t k = (uint32_t)s - before;                       // dead slots in [0, s)
+    if (k < np) lo[k] = (uint32_t)s;
+  } else if (live && s >= lnew) {
+    hi[before - lbl] = (uint32_t)s;
+  }
+}
+
+__global__ void cmp_swap(Params P, const uint32_t* cm, const uint32_t* lo, const uint32_t* hi) {
+  const uint32_t np = cm[CM_NPAIRS];
+  for (uint32_t k = blockIdx.x; k < np; k += gridDim.x) swap_slots(P, lo[k], hi[k], threadIdx.x);
+}
+
+__global__ void cmp_freeze(Params P, uint32_t* cm, uint32_t t) {
+  const uint64_t s = (uint64_t)blockIdx.x * CB + threadIdx.x;
+  if (s >= cm[CM_LNEW] && s < cm[CM_BOUND]) P.frz[s] = t;
+}
+__global__ void cmp_setbound(uint32_t* cm) { cm[CM_BOUND] = cm[CM_LNEW]; }
+
+__global__ void swap_one(Params P, uint64_t p, uint64_t q) { swap_slots(P, p, q, threadIdx.x); }
+
+// Wake: the link fault process of slots [s0, s1) over the steps they were frozen
+__global__ void replay_kernel(Params P, uint64_t s0, uint64_t s1, uint32_t tnow) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t c = s0 + i / P.N;
+  if (c >= s1) return;
+  Rep<0> x;
+  x.r = (uint32_t)(i % P.N);
+  x.c = c;
+  x.kc = P.kc[c];
+  const uint32_t poison =
+      reinterpret_cast<const uint32_t*>(P.image + (c / LANES) * (size_t)P.img.bytes + P.img.off_poison)[c % LANES];
+  uint32_t du[Rep<0>::NL], su[Rep<0>::NL];
+  for (uint32_t d = 0; d < Rep<0>::NL; d++) {
+    du[d] = d < P.N ? P.link_drop[krc(P, d, x.r, c)] : 0u;
+    su[d] = d < P.N ? P.link_slow[krc(P, d, x.r, c)] : 0u;
+  }
+  for (uint32_t t = P.frz[c]; t < tnow && t <= poison; t++) {   // the step kernel's gate: poison >= t
+    x.t = t;
+    x.hs = step_key(x.kc, t);
+    fault_process<0>(P, x, du, su);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -432,6 +633,8 @@ extern "C" int paxisim_destroy(paxisim* h) {
   if (h->arena) (void)hipFree(h->arena);
   if (h->d_faults) (void)hipFree(h->d_faults);
   if (h->d_scratch) (void)hipFree(h->d_scratch);
+  if (h->d_cmp) (void)hipFree(h->d_cmp);
+  if (h->d_pairs) (void)hipFree(h->d_pairs);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;
@@ -582,6 +785,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     uint32_t* wpend = carve<uint32_t>(p, wp ? NIC * PMAX : 0);
     uint4* wpx = carve<uint4>(p, wp && cfg->policy != PAXISIM_POLICY_CONSECUTIVE ? NIC * 3 : 0);
     uint4* hist = carve<uint4>(p, NC * P.H);
+    uint32_t* maps = carve<uint32_t>(p, C * 4);
     uint8_t* image = carve<uint8_t>(p, blocks * P.img.bytes);
     char* zend = p;
     uint4* rec = carve<uint4>(p, blocks * P.rec_per_block);
@@ -592,6 +796,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
       P.link_drop = links; P.link_slow = links + NC * N;
       P.ck_e = cke; P.ck_d = ckd; P.stats = st; P.reqx = reqx; P.hist = hist; P.image = image; P.rec = rec;
       P.wst = wst; P.wlog = wlog; P.wpend = wpend; P.gst = gst; P.wpx = wpx;
+      P.slot_of = maps; P.cl_of = maps + C; P.frz = maps + 2 * C; P.qf = maps + 3 * C;
     }
     return std::make_pair((size_t)zend, (size_t)p);
   };
@@ -608,15 +813,28 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
   h->arena_bytes = total;
   layout((char*)h->arena, true);
   int rc1 = 0;
+  const size_t ncmp = CM_SUMS + (cfg->clusters + CB - 1) / CB;
   if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipMalloc(&h->d_scratch, sizeof(uint64_t) * 64)) != hipSuccess ||
+      (e = hipMalloc(&h->d_cmp, sizeof(uint32_t) * ncmp)) != hipSuccess ||
+      (e = hipMalloc(&h->d_pairs, sizeof(uint32_t) * 2 * (C / 2 + LANES))) != hipSuccess ||
       (e = hipMalloc(&h->d_faults, sizeof(paxisim_fault) * PAXISIM_MAX_FAULTS)) != hipSuccess ||
       (e = hipMemsetAsync(h->arena, 0, zero_bytes, h->stream)) != hipSuccess)
     rc1 = fail(PAXISIM_EDEVICE, "device setup failed: %s", hipGetErrorString(e));
   if (!rc1) {
     P.faults = h->d_faults;
-    init_kernel<<<(unsigned)((C + 255) / 256), 256, 0, h->stream>>>(P);
-    if ((e = hipGetLastError()) != hipSuccess || (e = hipStreamSynchronize(h->stream)) != hipSuccess)
+    P.bound = h->d_cmp;
+    // compaction: Paxos (the swap covers its arrays); PAXISIM_COMPACT=0 turns it off (A/B)
+    const char* ce = getenv("PAXISIM_COMPACT");
+    P.compact = cfg->protocol == PAXISIM_PAXOS && !(ce && atoi(ce) == 0);
+    if (const char* ev = getenv("PAXISIM_COMPACT_EVERY")) h->cmp_every = (uint32_t)atoi(ev) ? (uint32_t)atoi(ev) : 1u;
+    for (uint32_t w = 0; w < wl->outstanding; w++)
+      if (P.start_step[w] + 1u > h->late_until) h->late_until = P.start_step[w] + 1u;
+    const uint32_t b0 = (uint32_t)cfg->clusters;
+    h->bound_host = b0;
+    e = hipMemcpyAsync(h->d_cmp, &b0, sizeof b0, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) init_kernel<<<(unsigned)((C + 255) / 256), 256, 0, h->stream>>>(P);
+    if (e != hipSuccess || (e = hipGetLastError()) != hipSuccess || (e = hipStreamSynchronize(h->stream)) != hipSuccess)
       rc1 = fail(PAXISIM_EDEVICE, "init kernel failed: %s", hipGetErrorString(e));
   }
   if (rc1) {
@@ -653,6 +871,56 @@ static hipError_t launch_any(paxisim* h, uint32_t t0, uint32_t n) {
   return h->ops.launch(h->P, h->stream, t0, n);
 }
 
+static int compact(paxisim* h) {
+  const Params& P = h->P;
+  const unsigned nb = (unsigned)((h->cfg.clusters + CB - 1) / CB);
+  uint32_t* lo = h->d_pairs;
+  uint32_t* hi = h->d_pairs + (P.C / 2 + LANES);
+  cmp_count<<<nb, CB, 0, h->stream>>>(P, h->d_cmp);
+  cmp_scan<<<1, CB, 0, h->stream>>>(P, h->d_cmp, nb);
+  cmp_index<<<nb, CB, 0, h->stream>>>(P, h->d_cmp, lo, hi);
+  cmp_swap<<<4096, LANES, 0, h->stream>>>(P, h->d_cmp, lo, hi);
+  cmp_freeze<<<nb, CB, 0, h->stream>>>(P, h->d_cmp, h->t);
+  cmp_setbound<<<1, 1, 0, h->stream>>>(h->d_cmp);
+  HIPCHK(hipGetLastError());
+  h->last_cmp = h->t;
+  return 0;
+}
+
+// A request for a frozen cluster: move it to the first frozen slot, replay the
+// fault process of that slot's tile up to now and step the tile again.
+static int wake(paxisim* h, uint64_t cluster) {
+  const Params& P = h->P;
+  uint32_t bound = 0, slot = 0;
+  HIPCHK(hipMemcpyAsync(&bound, h->d_cmp + CM_BOUND, 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(&slot, P.slot_of + cluster, 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->bound_host = bound;
+  if (slot < bound) return 0;
+  if (slot != bound) swap_one<<<1, LANES, 0, h->stream>>>(P, bound, slot);
+  uint64_t end = (uint64_t)bound + LANES;
+  if (end > h->cfg.clusters) end = h->cfg.clusters;
+  const uint64_t n = (end - bound) * P.N;
+  replay_kernel<<<(unsigned)((n + 63) / 64), 64, 0, h->stream>>>(P, bound, end, h->t);
+  const uint32_t nb32 = (uint32_t)end;
+  HIPCHK(hipMemcpyAsync(h->d_cmp + CM_BOUND, &nb32, 4, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->bound_host = nb32;
+  return 0;
+}
+
+extern "C" int paxisim_active_clusters(paxisim* h, uint64_t* active) {
+  if (!h || !active) return fail(PAXISIM_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  uint32_t bound = 0;
+  HIPCHK(hipMemcpyAsync(&bound, h->d_cmp + CM_BOUND, 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->bound_host = bound;
+  *active = bound;
+  return 0;
+}
+
 extern "C" int paxisim_step(paxisim* h, uint32_t nsteps) {
   if (!h) return fail(PAXISIM_EINVAL, "null handle");
   if ((uint64_t)h->t + nsteps >= T_MAX) return fail(PAXISIM_EINVAL, "step counter would exceed 2^28");
@@ -677,6 +945,10 @@ extern "C" int paxisim_step(paxisim* h, uint32_t nsteps) {
     h->launches++;
     h->t += n;
     nsteps -= n;
+    if (h->P.compact && h->t >= h->late_until && h->t - h->last_cmp >= h->cmp_every) {
+      const int rc = compact(h);
+      if (rc) return rc;
+    }
     if (h->evs.size() >= 256) {
       int rc = flush_events(h);
       if (rc) return rc;
@@ -712,6 +984,10 @@ extern "C" int paxisim_inject(paxisim* h, uint64_t cluster, uint32_t replica, ui
     return fail(PAXISIM_EINVAL, "bad inject (cluster %llu, replica %u, cid %u)", (unsigned long long)cluster,
                 replica, cid);
   HIPCHK(hipSetDevice(h->cfg.device));
+  if (h->P.compact) {
+    const int rc = wake(h, cluster);
+    if (rc) return rc;
+  }
   uint32_t st = 0;
   inject_kernel<<<1, 64, 0, h->stream>>>(h->P, cluster, replica, h->t % h->P.D, cid, (uint32_t*)h->d_scratch);
   HIPCHK(hipGetLastError());

@@ -126,7 +126,21 @@ struct Params {
   uint8_t* image;        // [blk][img.bytes]
   unsigned long long* dbg;  // diagnostic build only (PXS_STAMPS): per-wave phase totals
   uint4* rec;            // [blk][D][dst][src][M][64]
+  // Live-cluster compaction.  Every per-cluster array above is
+  // indexed by the cluster's *slot*; slot_of / cl_of map local cluster ids to
+  // slots and back.  Slots >= *bound hold quiescent (frozen) clusters that no
+  // launch touches; frz[s] is the step a frozen slot stopped at, qf[s] = 1 when
+  // the slot ended its last launch with an empty mailbox (a fixed point).
+  uint32_t* slot_of;     // [C] cluster -> slot
+  uint32_t* cl_of;       // [C] slot -> cluster
+  uint32_t* frz;         // [C] per slot
+  uint32_t* qf;          // [C] per slot
+  uint32_t* bound;       // device scalar: slots [0, *bound) are stepped
+  uint32_t compact;      // protocol supports compaction and it is enabled
 };
+
+// slot of local cluster c
+__device__ __forceinline__ uint64_t slot_of(const Params& P, uint64_t c) { return P.slot_of[c]; }
 
 // ---- PRNG ------------------------------------------------
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {

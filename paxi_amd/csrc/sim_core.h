@@ -624,6 +624,10 @@ template <int NT> constexpr int max_threads() {
 template <int NT, class Proto>
 __global__ void __launch_bounds__(max_threads<NT>(), min_waves<NT>()) sim_steps(Params P, uint32_t t0, uint32_t nsteps) {
   extern __shared__ uint4 lds[];
+  // slots [bound, C) hold frozen clusters: a workgroup wholly
+  // beyond the bound has nothing to do
+  const uint32_t bound = __builtin_amdgcn_readfirstlane(*P.bound);
+  if ((uint64_t)blockIdx.x * P.G * LANES >= bound) return;
   const uint32_t N = nrep<NT>(P);
   const uint32_t wave = threadIdx.x >> 6;
   const uint32_t grp = wave / N;
@@ -645,7 +649,7 @@ __global__ void __launch_bounds__(max_threads<NT>(), min_waves<NT>()) sim_steps(
   if (x.r >= N) x.r -= N;
   x.blk = blk;
   x.c = (uint64_t)blk * LANES + x.lane;
-  x.gid = P.cluster_base + x.c;
+  x.gid = P.cluster_base + P.cl_of[x.c];
   x.l_a = reinterpret_cast<uint32_t*>(L + P.img.off_a);
   x.l_b = reinterpret_cast<uint32_t*>(L + P.img.off_b);
   x.l_c = reinterpret_cast<uint32_t*>(L + P.img.off_c);
@@ -654,7 +658,7 @@ __global__ void __launch_bounds__(max_threads<NT>(), min_waves<NT>()) sim_steps(
   x.l_poison = reinterpret_cast<uint32_t*>(L + P.img.off_poison);
   x.l_cnt = L + P.img.off_cnt;
   x.rec = P.rec + (size_t)blk * P.rec_per_block;
-  const bool live = x.c < P.clusters && x.r < N;
+  const bool live = x.c < bound && x.r < N;
   if (live) {
     const size_t i = rc(P, x.r, x.c);
     x.kc = P.kc[x.c];
@@ -713,6 +717,14 @@ __global__ void __launch_bounds__(max_threads<NT>(), min_waves<NT>()) sim_steps(
   }
 #endif
 
+  // a cluster whose mailboxes are all empty after the launch is at a fixed
+  // point: nothing in it changes until a request is injected (compaction)
+  if (P.compact && live && x.r == 0) {
+    uint32_t any = 0;
+    const uint32_t nbox = P.D * N * (N + 1u);
+    for (uint32_t b = 0; b < nbox; b++) any |= x.l_cnt[(b << 6) | x.lane];
+    P.qf[x.c] = any ? 0u : 1u;
+  }
   {
     const uint32_t nb = P.img.bytes / 16u;
     uint4* g = reinterpret_cast<uint4*>(P.image + (size_t)blockIdx.x * P.G * P.img.bytes);

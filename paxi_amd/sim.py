@@ -46,6 +46,8 @@ def load_library():
                                   C.POINTER(C.c_uint32)]
     L.paxisim_occupancy.restype = C.c_int
     L.paxisim_occupancy.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+    L.paxisim_active_clusters.restype = C.c_int
+    L.paxisim_active_clusters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     L.paxisim_device_bytes.restype = C.c_int
     L.paxisim_device_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     if L.paxisim_abi_version() != abi.ABI_VERSION:
@@ -58,7 +60,7 @@ EXPORTED = ["paxisim_abi_version", "paxisim_last_error", "paxisim_create", "paxi
             "paxisim_fault_add", "paxisim_step", "paxisim_sync", "paxisim_stats_get",
             "paxisim_read_state", "paxisim_read_instances", "paxisim_check", "paxisim_kernel_time", "paxisim_device_bytes",
             "paxisim_linearizable", "paxisim_history", "paxisim_occupancy", "paxisim_inject", "paxisim_read_log",
-            "paxisim_history_load"]
+            "paxisim_history_load", "paxisim_active_clusters"]
 
 
 def _check(rc):
@@ -151,6 +153,12 @@ class Simulation:
         b, lds, j = C.c_int(), C.c_uint32(), C.c_uint32()
         _check(load_library().paxisim_occupancy(self.h, C.byref(b), C.byref(lds), C.byref(j)))
         return b.value, lds.value, j.value
+
+    def active_clusters(self):
+        """Clusters the step kernels still visit (the rest are frozen at a fixed point)."""
+        b = C.c_uint64()
+        _check(load_library().paxisim_active_clusters(self.h, C.byref(b)))
+        return b.value
 
     def device_bytes(self):
         b = C.c_uint64()
