@@ -629,7 +629,7 @@ __global__ void __launch_bounds__(max_threads<NT>(), min_waves<NT>()) sim_steps(
   const uint32_t bound = __builtin_amdgcn_readfirstlane(*P.bound);
   if ((uint64_t)blockIdx.x * P.G * LANES >= bound) return;
   const uint32_t N = nrep<NT>(P);
-  const uint32_t wave = threadIdx.x >> 6;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: keeps replica/tile state in SGPRs
   const uint32_t grp = wave / N;
   const uint32_t blk = blockIdx.x * P.G + grp;
   {
