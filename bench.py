@@ -273,6 +273,14 @@ def main():
     base, count = pdist.shard(args.clusters, rank)
     cfg, wl, fp, faults, desc = workload(args.config, count, base, local, args)
     sim = Simulation(cfg, wl, fp, faults)
+    pd = None
+    if world > 1 and backend == "nccl":
+        # the statistics go through the library's own RCCL communicator
+        # (paxisim_dist_init_rank); torch.distributed only ships its id
+        from paxi_amd.sim import Dist
+        uid = [Dist.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        pd = Dist.join(sim, uid[0], world, rank)
     for _ in range(args.warmup):
         sim.step(args.sim_steps)
     sim.sync()
@@ -298,9 +306,13 @@ def main():
         a, n, skipped = sim.linearizable()
         lin = {"anomalies": a, "ops_checked": n, "partitions_skipped": skipped, "scan_s": time.perf_counter() - tl}
 
-    tot, (dt_max, kms_max) = pdist.reduce_counters(
-        pdist.stats_counters(d, alg_bytes(d), violations, s1["flagged"]), [dt, kms],
-        device="cuda" if backend == "nccl" else "cpu")
+    st1 = sim.stats()
+    vals = pdist.stats_counters(d, alg_bytes(d), violations, s1["flagged"], agree_compared=st1.agree_compared,
+                                agree_missed=st1.agree_missed, active=sim.active_clusters())
+    if pd is not None:
+        tot, (dt_max, kms_max) = pdist.reduce_counters_abi(pd, vals, [dt, kms])
+    else:
+        tot, (dt_max, kms_max) = pdist.reduce_counters(vals, [dt, kms], device="cuda" if backend == "nccl" else "cpu")
 
     if rank == 0:
         avg_launch_ms = kms / max(1, launches)
@@ -329,6 +341,10 @@ def main():
             "commits_per_s": tot["commits"] / dt_max,
             "sim_steps_per_s": args.sim_steps * args.steps / dt_max,
             "agreement_violations": int(tot["violations"]),
+            "agreement_coverage": {"checkpoints_compared": int(tot["agree_compared"]),
+                                   "checkpoints_missed": int(tot["agree_missed"]),
+                                   "every": "16 executed slots, against the first executor (paxisim_check)"},
+            "active_clusters_end": int(tot["active"]),
             "unfaithful_clusters": int(tot["flag_UNFAITHFUL"]),
             "poisoned_clusters": int(tot["flag_POISON"]),
             "flagged_clusters": {n: int(tot["flag_" + n]) for n in FLAG_NAMES},
@@ -351,6 +367,8 @@ def main():
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
+    if pd is not None:
+        pd.close()
     sim.close()
     if world > 1:
         dist.destroy_process_group()

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PAXISIM_ABI_VERSION 7
+#define PAXISIM_ABI_VERSION 8
 
 #define PAXISIM_MAX_N        16  /* replicas per cluster (ack masks are u16) */
 #define PAXISIM_MAX_ZONES    16
@@ -148,6 +148,10 @@ typedef struct paxisim_config {
   uint32_t policy;            /* enum paxisim_policy: config.Policy */
   uint32_t policy_interval;   /* MAJORITY: config.Threshold seconds, in steps (>= 1) */
   double   policy_alpha;      /* EMA: config.Threshold, in (0, 1] */
+  uint32_t agree_ring;        /* agreement scan: digest checkpoints (every 16 executed slots) kept per
+                                 cluster and instance, i.e. the lag in slots / 16 it can bridge;
+                                 0 = default (Paxos 1024, WPaxos 128, ABD none) */
+  uint32_t pad0;
 } paxisim_config;
 
 /* Key distributions of the benchmark's key generator (benchmark.go:202-244,
@@ -243,6 +247,10 @@ typedef struct paxisim_stats {
   uint64_t commits;           /* committed slots (the second metric) */
   uint64_t replies;
   uint64_t flagged[8];        /* clusters with flag bit i set */
+  /* agreement scan coverage (paxisim_check): a replica reaching a digest
+   * checkpoint (every 16 executed slots) compares it with the first replica's
+   * digest there; `missed` = the first digest had already left the ring */
+  uint64_t agree_compared, agree_missed, agree_mismatch;
 } paxisim_stats;
 
 /* One log entry (read_log): paxos/paxos.go:11-18 entry of a slot in the
@@ -309,7 +317,11 @@ int  paxisim_read_log(paxisim* h, uint64_t cluster, uint32_t replica, uint32_t k
 
 /* Agreement scan (client.go:279-320 / tla Safety): number of clusters in
  * which two replicas executed different commands in the same slot (of the
- * same key, for WPaxos). */
+ * same key, for WPaxos).  Every replica's executed prefix is compared with
+ * the first executor's at each 16-slot checkpoint as it is reached, however
+ * far behind it runs (up to agree_ring checkpoints); replicas at the same
+ * execute count, and the last 8 checkpoints of every pair, are compared here.
+ * Coverage is in paxisim_stats.agree_*. */
 int  paxisim_check(paxisim* h, uint64_t* violations);
 
 /* Device time of the step kernels since the last reset (HIP events on the
@@ -348,6 +360,27 @@ int  paxisim_active_clusters(paxisim* h, uint64_t* active);
 
 /* Bytes of device memory held by the handle. */
 int  paxisim_device_bytes(paxisim* h, uint64_t* bytes);
+
+/* ---- Multi-GPU: clusters shard by range over handles
+ * (paxisim_config.cluster_base = rank * clusters), the simulation itself has
+ * no collective, and totals are reduced with RCCL (opened at run time:
+ * EUNSUPP without librccl.so.1).  Replaces nothing in the reference, which
+ * simulates one cluster per process. */
+typedef struct paxisim_dist paxisim_dist;
+/* One process driving one handle per device: a communicator clique. */
+int  paxisim_dist_init(paxisim* const* handles, int n, paxisim_dist** out);
+/* One handle per process: one rank gets an id, the caller ships its 128 bytes
+ * to every rank, and each rank joins with it. */
+int  paxisim_dist_unique_id(unsigned char id[128]);
+int  paxisim_dist_init_rank(paxisim* h, const unsigned char id[128], int nranks, int rank, paxisim_dist** out);
+/* Sum n u64 values and max m doubles over every handle of every rank; member
+ * k of this process supplies sums_in[k*n..] and maxes_in[k*m..] (n, m <= 64). */
+int  paxisim_dist_allreduce(paxisim_dist* d, const uint64_t* sums_in, uint32_t n, const double* maxes_in,
+                            uint32_t m, uint64_t* sums_out, double* maxes_out);
+/* paxisim_stats summed over every handle of the job (flagged[] are cluster
+ * counts, so they sum too), and the largest step-kernel time (may be NULL). */
+int  paxisim_dist_stats(paxisim_dist* d, paxisim_stats* out, double* kernel_ms_max);
+int  paxisim_dist_destroy(paxisim_dist* d);
 
 #ifdef __cplusplus
 }

@@ -194,6 +194,7 @@ typedef struct replica {
   /* counters */
   uint32_t delivered[PAXISIM_NMSG];
   uint32_t client_requests, sent, dropped, discarded, commits, replies;
+  uint32_t agc, agm, agb;          /* agreement checkpoints compared / missed / mismatched */
   /* ABD (abd/replica.go:28-34): cid counter, versioned KV, op table */
   uint32_t abd_cid;
   uint32_t *kv_val, *kv_ver;
@@ -209,6 +210,7 @@ typedef struct cluster {
   uint32_t wk_cur[PAXISIM_MAX_WORKERS], wk_issued[PAXISIM_MAX_WORKERS];
   replica_t rep[PAXISIM_MAX_N];
   rec_t* mbox;                     /* [D][N][N+1][M] */
+  uint64_t* agr;                   /* [NK][AR] first executor's digest per checkpoint: k << 40 | fold */
   uint8_t* cnt;                    /* [D][N][N+1] */
 } cluster_t;
 
@@ -228,6 +230,7 @@ struct oracle_sim {
   uint32_t NK;                     /* Paxos instances per replica: WPaxos keys, else 1 */
   uint32_t q1, q2;                 /* quorum kinds in use (WPaxos: from fz, wpaxos/kpaxos.go:16-28) */
   uint32_t late_workers;           /* some worker has start_step > 0 */
+  uint32_t AR;                     /* agreement ring: checkpoints kept per (cluster, instance) */
 };
 
 /* handler context: one replica of one cluster at one step */
@@ -530,6 +533,7 @@ static void replica_handle_request(ctx_t* x, uint32_t req) {
 }
 
 static void paxos_exec(ctx_t* x);
+static void agree_arrive(ctx_t* x, uint32_t k);
 
 static void paxos_handle_p1a(ctx_t* x, uint32_t mb) {      /* paxos.go:134-162 */
   inst_t* p = x->p;
@@ -717,6 +721,23 @@ static void paxos_handle_p3(ctx_t* x, uint32_t mb, int32_t ms, uint32_t mcid) { 
   if (!x->s->cfg.reply_when_commit) paxos_exec(x);
 }
 
+/* Agreement as a running check (client.go:279-320 Consensus: per index the
+ * executed values form a set of size <= 1): the first replica to reach digest
+ * checkpoint k (every CKI executed slots) records it in the cluster's ring,
+ * every later one compares.  Which replica is first does not change whether
+ * some pair disagrees, so this equals the device's concurrent version. */
+static void agree_arrive(ctx_t* x, uint32_t k) {
+  const uint32_t key = (uint32_t)(x->p - x->n->inst);
+  uint64_t* a = &x->c->agr[(size_t)key * x->s->AR + k % x->s->AR];
+  const uint64_t d = x->p->digest;
+  const uint64_t want = ((uint64_t)k << 40) | ((d ^ (d >> 24)) & 0xFFFFFFFFFFull);
+  const uint32_t tv = (uint32_t)(*a >> 40);
+  if (*a == 0 || tv < k) { *a = want; return; }
+  if (tv > k) { x->n->agm++; return; }                      /* the first digest has left the ring */
+  x->n->agc++;
+  if (*a != want) x->n->agb++;
+}
+
 static void paxos_exec(ctx_t* x) {                         /* paxos.go:345-369 */
   inst_t* p = x->p;
   for (;;) {
@@ -741,6 +762,7 @@ static void paxos_exec(ctx_t* x) {                         /* paxos.go:345-369 *
       uint32_t k = ((uint32_t)p->execute / CKI) % CKR;
       p->ck_e[k] = (uint32_t)p->execute;
       p->ck_d[k] = p->digest;
+      if (x->s->AR) agree_arrive(x, (uint32_t)p->execute / CKI);
     }
   }
 }
@@ -1175,6 +1197,7 @@ static int check_config(const paxisim_config* cfg, const paxisim_workload* wl,
   if (cfg->max_delay > PAXISIM_MAX_DELAY) return fail(PAXISIM_EINVAL, "max_delay");
   if (cfg->q1 > PAXISIM_Q_FGRID_Q2 || cfg->q2 > PAXISIM_Q_FGRID_Q2) return fail(PAXISIM_EINVAL, "quorum kind");
   if (cfg->clusters < 1) return fail(PAXISIM_EINVAL, "clusters");
+  if (cfg->agree_ring > 65536) return fail(PAXISIM_EINVAL, "agree_ring > 65536");
   if (wl->outstanding < 1 || wl->outstanding > PAXISIM_MAX_WORKERS) return fail(PAXISIM_EINVAL, "outstanding");
   if (wl->outstanding > cfg->mbox_cap) return fail(PAXISIM_EINVAL, "outstanding exceeds mbox_cap");
   if (wl->distribution > PAXISIM_DIST_TABLE) return fail(PAXISIM_EINVAL, "distribution %u", wl->distribution);
@@ -1260,6 +1283,8 @@ int oracle_create(const paxisim_config* cfg, const paxisim_workload* wl,
   for (z = 0; z < s->wl.outstanding; z++) s->late_workers |= s->wl.start_step[z] != 0;
   s->OW = abd_ow(wl->outstanding);
   s->NK = cfg->protocol == PAXISIM_WPAXOS ? cfg->keys : 1u;
+  s->AR = cfg->protocol == PAXISIM_ABD ? 0u
+          : cfg->agree_ring ? cfg->agree_ring : (cfg->protocol == PAXISIM_WPAXOS ? 128u : 1024u);
   s->q1 = cfg->q1;
   s->q2 = cfg->q2;
   if (cfg->protocol == PAXISIM_WPAXOS) {
@@ -1278,12 +1303,14 @@ int oracle_create(const paxisim_config* cfg, const paxisim_workload* wl,
     inst_t* insts = (inst_t*)calloc((size_t)N * s->NK, sizeof(inst_t));
     c->mbox = (rec_t*)malloc((size_t)s->D * N * s->NS * s->M * sizeof(rec_t));
     c->cnt = (uint8_t*)calloc((size_t)s->D * N * s->NS, 1);
-    if (!logs || !insts || !c->mbox || !c->cnt) {
+    c->agr = s->AR ? (uint64_t*)calloc((size_t)s->NK * s->AR, sizeof(uint64_t)) : NULL;
+    if (!logs || !insts || !c->mbox || !c->cnt || (s->AR && !c->agr)) {
       free(logs);
       free(insts);
       s->C = i;
       free(c->mbox);
       free(c->cnt);
+      free(c->agr);
       oracle_destroy(s);
       return fail(PAXISIM_ENOMEM, "oom");
     }
@@ -1314,6 +1341,7 @@ int oracle_destroy(oracle_sim* s) {
     }
     free(c->mbox);
     free(c->cnt);
+    free(c->agr);
   }
   free(s->cl);
   free(s);
@@ -1536,6 +1564,9 @@ int oracle_stats_get(oracle_sim* s, paxisim_stats* o) {
       o->discarded += p->discarded;
       o->commits += p->commits;
       o->replies += p->replies;
+      o->agree_compared += p->agc;
+      o->agree_missed += p->agm;
+      o->agree_mismatch += p->agb;
       cf |= p->flags;
     }
     for (k = 0; k < 8; k++) if (cf & (1u << k)) o->flagged[k]++;
@@ -1553,6 +1584,7 @@ int oracle_check(oracle_sim* s, uint64_t* violations) {
     const cluster_t* c = &s->cl[i];
     int bad = 0;
     uint32_t key;
+    for (a = 0; a < s->N; a++) bad |= c->rep[a].agb != 0;      /* running check (agree_arrive) */
     for (key = 0; key < s->NK && !bad; key++)      /* per Paxos instance: WPaxos per key (tla Safety) */
       for (a = 0; a < s->N && !bad; a++)
         for (b = a + 1; b < s->N && !bad; b++) {

@@ -6,7 +6,7 @@ structs, so the two speak exactly the same ABI.
 """
 import ctypes as C
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 MAX_N = 16
 MAX_ZONES = 16
 MAX_WORKERS = 32
@@ -75,6 +75,7 @@ class Config(C.Structure):
         ("policy", C.c_uint32),
         ("policy_interval", C.c_uint32),
         ("policy_alpha", C.c_double),
+        ("agree_ring", C.c_uint32), ("pad0", C.c_uint32),
     ]
 
 
@@ -168,11 +169,13 @@ class Stats(C.Structure):
         ("sent", C.c_uint64), ("dropped", C.c_uint64), ("discarded", C.c_uint64),
         ("commits", C.c_uint64), ("replies", C.c_uint64),
         ("flagged", C.c_uint64 * 8),
+        ("agree_compared", C.c_uint64), ("agree_missed", C.c_uint64), ("agree_mismatch", C.c_uint64),
     ]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k in ("steps", "clusters", "delivered_total", "client_requests",
-                                            "sent", "dropped", "discarded", "commits", "replies")}
+                                            "sent", "dropped", "discarded", "commits", "replies",
+                                            "agree_compared", "agree_missed", "agree_mismatch")}
         d["delivered"] = {MSG_NAMES.get(i, str(i)): self.delivered[i] for i in range(NMSG) if self.delivered[i]}
         d["flagged"] = list(self.flagged)
         return d
@@ -206,7 +209,7 @@ def make_config(npz=(5,), protocol=PAXOS, q1=Q_MAJORITY, q2=Q_MAJORITY, fz=0, th
                 ephemeral_leader=0, reply_when_commit=0, adaptive=1, policy_threshold=3,
                 window=16, mbox_cap=16, max_delay=4, keys=16, steps_per_launch=0, device=0,
                 clusters=1, cluster_base=0, seed=1, history=0, policy=POLICY_CONSECUTIVE, policy_interval=1,
-                policy_alpha=0.5):
+                policy_alpha=0.5, agree_ring=0):
     c = Config()
     c.protocol = protocol
     c.n_zones = len(npz)
@@ -219,6 +222,7 @@ def make_config(npz=(5,), protocol=PAXOS, q1=Q_MAJORITY, q2=Q_MAJORITY, fz=0, th
     c.steps_per_launch, c.device, c.history = steps_per_launch, device, history
     c.clusters, c.cluster_base, c.seed = clusters, cluster_base, seed
     c.policy, c.policy_interval, c.policy_alpha = policy, policy_interval, policy_alpha
+    c.agree_ring = agree_ring
     return c
 
 

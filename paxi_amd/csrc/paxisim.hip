@@ -5,6 +5,9 @@
 // PAXISIM_EDEVICE.
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -266,6 +269,7 @@ __global__ void check_kernel(Params P, uint64_t* out) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t bad = 0;
   if (c < P.clusters) {
+    for (uint32_t r = 0; r < P.N; r++) bad |= P.stats[krc(P, ST_AGB, r, c)] != 0;   // running check (paxos_exec)
     auto exec_digest = [&](uint32_t key, uint32_t r, uint32_t& e, uint64_t& d) {
       if (P.protocol == PAXISIM_WPAXOS) {
         const size_t si = (((c / LANES) * P.keys + key) * P.N + r) * LANES + (c % LANES);
@@ -412,6 +416,7 @@ __device__ void swap_slots(const Params& P, uint64_t p, uint64_t q, uint32_t j) 
   swap_rows(P.ck_d, (size_t)CKR * P.NI, C, p, q, j);
   swap_rows(P.gst, (size_t)GMAX * P.NI, C, p, q, j);
   swap_rows(P.stats, (size_t)NSTAT * N, C, p, q, j);
+  swap_rows(P.agr, (size_t)P.AR * P.NK, C, p, q, j);
   swap_rows(P.frz, 1, C, p, q, j);
   swap_rows(P.qf, 1, C, p, q, j);
   swap_lanes(P.reqx, (size_t)N * P.W * LANES, (size_t)N * P.W, p, q, j);
@@ -586,6 +591,7 @@ static int check_config(const paxisim_config* cfg, const paxisim_workload* wl, c
   if (cfg->max_delay > PAXISIM_MAX_DELAY) return fail(PAXISIM_EINVAL, "max_delay");
   if (cfg->q1 > PAXISIM_Q_FGRID_Q2 || cfg->q2 > PAXISIM_Q_FGRID_Q2) return fail(PAXISIM_EINVAL, "quorum kind");
   if (cfg->clusters < 1) return fail(PAXISIM_EINVAL, "clusters");
+  if (cfg->agree_ring > 65536) return fail(PAXISIM_EINVAL, "agree_ring > 65536");
   if (wl->outstanding < 1 || wl->outstanding > PAXISIM_MAX_WORKERS) return fail(PAXISIM_EINVAL, "outstanding");
   if (wl->outstanding > cfg->mbox_cap) return fail(PAXISIM_EINVAL, "outstanding exceeds mbox_cap");
   if (wl->distribution > PAXISIM_DIST_TABLE) return fail(PAXISIM_EINVAL, "distribution %u", wl->distribution);
@@ -689,6 +695,8 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
   P.policy_interval = cfg->policy_interval;
   P.policy_alpha = cfg->policy_alpha;
   P.H = cfg->protocol == PAXISIM_ABD ? cfg->history : 0;
+  P.AR = cfg->protocol == PAXISIM_ABD ? 0u
+         : cfg->agree_ring ? cfg->agree_ring : (cfg->protocol == PAXISIM_WPAXOS ? 128u : 1024u);
   P.OW = abd_ow(wl->outstanding);
   P.W = cfg->window;
   P.M = cfg->mbox_cap;
@@ -786,6 +794,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     uint4* wpx = carve<uint4>(p, wp && cfg->policy != PAXISIM_POLICY_CONSECUTIVE ? NIC * 3 : 0);
     uint4* hist = carve<uint4>(p, NC * P.H);
     uint32_t* maps = carve<uint32_t>(p, C * 4);
+    unsigned long long* agr = carve<unsigned long long>(p, (size_t)P.AR * P.NK * C);
     uint8_t* image = carve<uint8_t>(p, blocks * P.img.bytes);
     char* zend = p;
     uint4* rec = carve<uint4>(p, blocks * P.rec_per_block);
@@ -797,6 +806,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
       P.ck_e = cke; P.ck_d = ckd; P.stats = st; P.reqx = reqx; P.hist = hist; P.image = image; P.rec = rec;
       P.wst = wst; P.wlog = wlog; P.wpend = wpend; P.gst = gst; P.wpx = wpx;
       P.slot_of = maps; P.cl_of = maps + C; P.frz = maps + 2 * C; P.qf = maps + 3 * C;
+      P.agr = agr;
     }
     return std::make_pair((size_t)zend, (size_t)p);
   };
@@ -1037,6 +1047,9 @@ extern "C" int paxisim_stats_get(paxisim* h, paxisim_stats* out) {
   out->discarded = red[ST_DISCARDED];
   out->commits = red[ST_COMMITS];
   out->replies = red[ST_REPLIES];
+  out->agree_compared = red[ST_AGC];
+  out->agree_missed = red[ST_AGM];
+  out->agree_mismatch = red[ST_AGB];
   for (int b = 0; b < 8; b++) out->flagged[b] = red[NSTAT + b];
   return 0;
 }
@@ -1198,6 +1211,210 @@ extern "C" int paxisim_linearizable(paxisim* h, uint64_t* anomalies, uint64_t* o
   if (anomalies) *anomalies = res[0];
   if (ops) *ops = res[1];
   if (skipped) *skipped = res[2];
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Multi-GPU behind the C-ABI: clusters shard by range across
+// handles (cluster_base), the data path has no collective, and the statistics
+// are summed (max for time) with one RCCL all-reduce.  RCCL is opened at run
+// time, so the library loads without it and only these calls need it; a
+// process that already holds librccl.so.1 (e.g. through torch) shares it.
+// ---------------------------------------------------------------------------
+namespace {
+struct Rccl {
+  bool ok = false;
+  ncclResult_t (*get_unique_id)(ncclUniqueId*);
+  ncclResult_t (*init_rank)(ncclComm_t*, int, ncclUniqueId, int);
+  ncclResult_t (*init_all)(ncclComm_t*, int, const int*);
+  ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+  ncclResult_t (*group_start)();
+  ncclResult_t (*group_end)();
+  ncclResult_t (*destroy)(ncclComm_t);
+  const char* (*error_string)(ncclResult_t);
+};
+Rccl& rccl() {
+  static Rccl r;
+  static bool tried = false;
+  if (tried) return r;
+  tried = true;
+  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) return r;
+  auto sym = [&](const char* n) { return dlsym(h, n); };
+  r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(sym("ncclGetUniqueId"));
+  r.init_rank = reinterpret_cast<decltype(r.init_rank)>(sym("ncclCommInitRank"));
+  r.init_all = reinterpret_cast<decltype(r.init_all)>(sym("ncclCommInitAll"));
+  r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(sym("ncclAllReduce"));
+  r.group_start = reinterpret_cast<decltype(r.group_start)>(sym("ncclGroupStart"));
+  r.group_end = reinterpret_cast<decltype(r.group_end)>(sym("ncclGroupEnd"));
+  r.destroy = reinterpret_cast<decltype(r.destroy)>(sym("ncclCommDestroy"));
+  r.error_string = reinterpret_cast<decltype(r.error_string)>(sym("ncclGetErrorString"));
+  r.ok = r.get_unique_id && r.init_rank && r.init_all && r.all_reduce && r.group_start && r.group_end && r.destroy &&
+         r.error_string;
+  return r;
+}
+}  // namespace
+
+#define RCCLCHK(expr)                                                                      \
+  do {                                                                                     \
+    ncclResult_t r_ = (expr);                                                              \
+    if (r_ != ncclSuccess) return fail(PAXISIM_EDEVICE, "%s: %s", #expr, rccl().error_string(r_)); \
+  } while (0)
+
+struct paxisim_dist {
+  std::vector<paxisim*> h;           // handles driven by this process, one per device
+  std::vector<ncclComm_t> comm;
+  std::vector<void*> buf;            // per member: device buffer for the reduction
+};
+
+constexpr uint32_t DIST_MAXV = 64;   // u64 sums + f64 maxes per reduction
+
+extern "C" int paxisim_dist_unique_id(unsigned char id[128]) {
+  if (!id) return fail(PAXISIM_EINVAL, "null argument");
+  if (!rccl().ok) return fail(PAXISIM_EUNSUPP, "RCCL (librccl.so.1) not available");
+  ncclUniqueId u;
+  RCCLCHK(rccl().get_unique_id(&u));
+  memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+  return 0;
+}
+
+static int dist_alloc(paxisim_dist* d) {
+  for (paxisim* h : d->h) {
+    void* b = nullptr;
+    HIPCHK(hipSetDevice(h->cfg.device));
+    HIPCHK(hipMalloc(&b, 2 * DIST_MAXV * sizeof(uint64_t)));
+    d->buf.push_back(b);
+  }
+  return 0;
+}
+
+extern "C" int paxisim_dist_destroy(paxisim_dist* d) {
+  if (!d) return 0;
+  for (size_t i = 0; i < d->comm.size(); i++) (void)rccl().destroy(d->comm[i]);
+  for (size_t i = 0; i < d->buf.size(); i++) {
+    (void)hipSetDevice(d->h[i]->cfg.device);
+    (void)hipFree(d->buf[i]);
+  }
+  delete d;
+  return 0;
+}
+
+// Single process, one handle per device (ncclCommInitAll)
+extern "C" int paxisim_dist_init(paxisim* const* handles, int n, paxisim_dist** out) {
+  if (!handles || n < 1 || !out) return fail(PAXISIM_EINVAL, "bad argument");
+  if (!rccl().ok) return fail(PAXISIM_EUNSUPP, "RCCL (librccl.so.1) not available");
+  std::vector<int> devs;
+  for (int i = 0; i < n; i++) {
+    if (!handles[i]) return fail(PAXISIM_EINVAL, "null handle %d", i);
+    for (int d : devs)
+      if (d == handles[i]->cfg.device) return fail(PAXISIM_EINVAL, "two handles on device %d", d);
+    devs.push_back(handles[i]->cfg.device);
+  }
+  paxisim_dist* d = new (std::nothrow) paxisim_dist();
+  if (!d) return fail(PAXISIM_ENOMEM, "oom");
+  d->h.assign(handles, handles + n);
+  d->comm.resize(n);
+  ncclResult_t r = rccl().init_all(d->comm.data(), n, devs.data());
+  if (r != ncclSuccess) {
+    d->comm.clear();
+    paxisim_dist_destroy(d);
+    return fail(PAXISIM_EDEVICE, "ncclCommInitAll: %s", rccl().error_string(r));
+  }
+  int rc = dist_alloc(d);
+  if (rc) {
+    paxisim_dist_destroy(d);
+    return rc;
+  }
+  *out = d;
+  return 0;
+}
+
+// One handle per process: every rank passes the id one rank obtained from
+// paxisim_dist_unique_id (the caller ships it, e.g. over its launcher)
+extern "C" int paxisim_dist_init_rank(paxisim* h, const unsigned char id[128], int nranks, int rank,
+                                      paxisim_dist** out) {
+  if (!h || !id || nranks < 1 || rank < 0 || rank >= nranks || !out) return fail(PAXISIM_EINVAL, "bad argument");
+  if (!rccl().ok) return fail(PAXISIM_EUNSUPP, "RCCL (librccl.so.1) not available");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  paxisim_dist* d = new (std::nothrow) paxisim_dist();
+  if (!d) return fail(PAXISIM_ENOMEM, "oom");
+  d->h.push_back(h);
+  d->comm.resize(1);
+  ncclUniqueId u;
+  memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+  ncclResult_t r = rccl().init_rank(&d->comm[0], nranks, u, rank);
+  if (r != ncclSuccess) {
+    d->comm.clear();
+    paxisim_dist_destroy(d);
+    return fail(PAXISIM_EDEVICE, "ncclCommInitRank: %s", rccl().error_string(r));
+  }
+  int rc = dist_alloc(d);
+  if (rc) {
+    paxisim_dist_destroy(d);
+    return rc;
+  }
+  *out = d;
+  return 0;
+}
+
+// Sum sums_in[i] (i < n) and max maxes_in[j] (j < m) over every member of
+// every rank; member k's inputs are at sums_in[k*n], maxes_in[k*m].  The
+// result (the same on every member) goes to sums_out[0..n), maxes_out[0..m).
+extern "C" int paxisim_dist_allreduce(paxisim_dist* d, const uint64_t* sums_in, uint32_t n, const double* maxes_in,
+                                      uint32_t m, uint64_t* sums_out, double* maxes_out) {
+  if (!d || n > DIST_MAXV || m > DIST_MAXV || (n && (!sums_in || !sums_out)) || (m && (!maxes_in || !maxes_out)))
+    return fail(PAXISIM_EINVAL, "bad argument");
+  const size_t k = d->h.size();
+  for (size_t i = 0; i < k; i++) {
+    paxisim* h = d->h[i];
+    HIPCHK(hipSetDevice(h->cfg.device));
+    uint64_t* b = static_cast<uint64_t*>(d->buf[i]);
+    if (n) HIPCHK(hipMemcpyAsync(b, sums_in + i * n, n * 8, hipMemcpyHostToDevice, h->stream));
+    if (m) HIPCHK(hipMemcpyAsync(b + DIST_MAXV, maxes_in + i * m, m * 8, hipMemcpyHostToDevice, h->stream));
+  }
+  RCCLCHK(rccl().group_start());
+  for (size_t i = 0; i < k; i++) {
+    uint64_t* b = static_cast<uint64_t*>(d->buf[i]);
+    if (n) (void)rccl().all_reduce(b, b, n, ncclUint64, ncclSum, d->comm[i], d->h[i]->stream);
+    if (m) (void)rccl().all_reduce(b + DIST_MAXV, b + DIST_MAXV, m, ncclFloat64, ncclMax, d->comm[i], d->h[i]->stream);
+  }
+  RCCLCHK(rccl().group_end());
+  for (size_t i = 0; i < k; i++) {
+    paxisim* h = d->h[i];
+    HIPCHK(hipSetDevice(h->cfg.device));
+    uint64_t* b = static_cast<uint64_t*>(d->buf[i]);
+    if (i == 0 && n) HIPCHK(hipMemcpyAsync(sums_out, b, n * 8, hipMemcpyDeviceToHost, h->stream));
+    if (i == 0 && m) HIPCHK(hipMemcpyAsync(maxes_out, b + DIST_MAXV, m * 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+  }
+  return 0;
+}
+
+// paxisim_stats summed over every handle of the job (u64 fields), and the
+// largest step-kernel time of any handle (kernel_ms_max may be NULL)
+extern "C" int paxisim_dist_stats(paxisim_dist* d, paxisim_stats* out, double* kernel_ms_max) {
+  if (!d || !out) return fail(PAXISIM_EINVAL, "null argument");
+  constexpr uint32_t NV = sizeof(paxisim_stats) / sizeof(uint64_t);
+  static_assert(sizeof(paxisim_stats) % sizeof(uint64_t) == 0 && NV <= DIST_MAXV, "stats layout");
+  const size_t k = d->h.size();
+  std::vector<uint64_t> in(k * NV);
+  std::vector<double> tin(k);
+  for (size_t i = 0; i < k; i++) {
+    paxisim_stats s;
+    int rc = paxisim_stats_get(d->h[i], &s);
+    if (rc) return rc;
+    memcpy(&in[i * NV], &s, sizeof s);
+    double ms = 0;
+    if ((rc = paxisim_kernel_time(d->h[i], &ms, nullptr, 0))) return rc;
+    tin[i] = ms;
+  }
+  uint64_t res[NV];
+  double tmax = 0;
+  int rc = paxisim_dist_allreduce(d, in.data(), NV, tin.data(), 1, res, &tmax);
+  if (rc) return rc;
+  memcpy(out, res, sizeof *out);
+  if (kernel_ms_max) *kernel_ms_max = tmax;
   return 0;
 }
 

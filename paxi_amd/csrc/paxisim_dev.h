@@ -43,6 +43,7 @@ enum {
   ST_DELIV0 = 0,                    // 16 slots: delivered by message type
   ST_CLIENT = PAXISIM_NMSG,
   ST_SENT, ST_DROPPED, ST_DISCARDED, ST_COMMITS, ST_REPLIES,
+  ST_AGC, ST_AGM, ST_AGB,           // agreement checkpoints compared / missed / mismatched
   NSTAT
 };
 
@@ -121,6 +122,8 @@ struct Params {
   uint32_t* wpend;       // [blk][K][N][64][PMAX]
   uint4* wpx;            // [blk][K][N][64][3] majority {hits u16 x 16 (2 x uint4), {sum, start step}} / ema {s lo, s hi, zone}
   uint32_t* stats;       // [NSTAT][N][C]
+  unsigned long long* agr;  // [AR][NK][C] first executor's digest per checkpoint: k << 40 | 40-bit digest fold
+  uint32_t AR;           // checkpoints kept per (cluster, instance); 0 = no agreement ring
   uint32_t* reqx;        // [blk][N][W][64] request side table (Paxos)
   uint4* hist;           // [N][C][H] completed ABD ops {key|write<<31, value, start, end}
   uint8_t* image;        // [blk][img.bytes]

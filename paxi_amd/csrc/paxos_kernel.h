@@ -255,6 +255,27 @@ __device__ __forceinline__ void handle_request(const Params& P, Rep<NT>& x, uint
   else node_forward<NT>(P, x, bal_id(x.ballot), req);
 }
 
+// Agreement ring (client.go:279-320 Consensus, restated as a running check):
+// the first replica to reach digest checkpoint k records it, every later one
+// compares (a 64-bit CAS, so concurrent arrivals in one step agree on who was
+// first; whether some pair disagrees does not depend on that order).
+static __device__ __noinline__ void agree_arrive(unsigned long long* a, uint32_t* st0, size_t sstride, uint32_t k,
+                                         uint64_t digest) {
+  const unsigned long long want = ((unsigned long long)k << 40) | ((digest ^ (digest >> 24)) & 0xFFFFFFFFFFull);
+  unsigned long long v = atomicCAS(a, 0ull, want);
+  uint32_t st = 0;                                       // 0: first to arrive, recorded
+  while (v != 0ull) {
+    const uint32_t tv = (uint32_t)(v >> 40);
+    if (tv == k) { st = v == want ? ST_AGC : ST_AGB; break; }
+    if (tv > k) { st = ST_AGM; break; }                  // the first digest has left the ring
+    const unsigned long long o = atomicCAS(a, v, want);  // an older checkpoint: claim the slot
+    if (o == v) break;
+    v = o;
+  }
+  if (st == ST_AGB) st0[ST_AGC * sstride] += 1;          // a mismatch was compared too
+  if (st) st0[st * sstride] += 1;
+}
+
 template <int NT>
 __device__ __forceinline__ void paxos_exec(const Params& P, Rep<NT>& x) {     // paxos.go:345-369
   for (;;) {
@@ -272,6 +293,11 @@ __device__ __forceinline__ void paxos_exec(const Params& P, Rep<NT>& x) {     //
       const size_t ci = ((size_t)k * P.NI + x.inst) * P.C + x.c;
       P.ck_e[ci] = (uint32_t)x.execute;
       P.ck_d[ci] = x.digest;
+      if (P.AR) {
+        const uint32_t kk = (uint32_t)x.execute / CKI;
+        agree_arrive(&P.agr[((size_t)(kk % P.AR) * P.NK + x.key) * P.C + x.c], &P.stats[rc(P, x.r, x.c)],
+                     (size_t)P.N * P.C, kk, x.digest);
+      }
     }
   }
 }
@@ -484,6 +510,7 @@ struct PaxosProto {
     // the replica's one instance: LDS log window [r][W][lane], SoA pending table
     x.iflags = x.flags & (PAXISIM_F_WOVF | PAXISIM_F_GHOST);
     x.inst = x.r;
+    x.key = 0;
     x.ktag = 0;
     x.e0 = ((x.r * P.W) << 6) | x.lane;
     x.es = LANES;

@@ -12,7 +12,7 @@ import os
 # order of the per-rank counter vector that gets all-reduced
 FLAG_NAMES = ("WOVF", "GHOST", "MBOX_OVF", "PEND_OVF", "UNFAITHFUL", "POISON", "BALLOT_OVF", "HIST_OVF")
 COUNTERS = ("delivered_total", "commits", "replies", "dropped", "client_requests", "alg_bytes",
-            "violations") + tuple("flag_" + n for n in FLAG_NAMES)
+            "violations", "agree_compared", "agree_missed", "active") + tuple("flag_" + n for n in FLAG_NAMES)
 
 
 def env_rank():
@@ -24,6 +24,13 @@ def env_rank():
 def shard(clusters_per_rank, rank):
     """Global cluster range of one rank under weak scaling: (cluster_base, count)."""
     return rank * clusters_per_rank, clusters_per_rank
+
+
+def reduce_counters_abi(pd, values, elapsed):
+    """The same reduction through the C-ABI (paxisim_dist_allreduce, RCCL):
+    integer sums and float maxes over every rank of the communicator `pd`."""
+    sums, maxes = pd.allreduce([[int(values.get(k, 0)) for k in COUNTERS]], [[float(e) for e in elapsed]])
+    return dict(zip(COUNTERS, [float(v) for v in sums])), maxes
 
 
 def reduce_counters(values, elapsed, device=None, group=None):
@@ -39,11 +46,13 @@ def reduce_counters(values, elapsed, device=None, group=None):
     return dict(zip(COUNTERS, vec.tolist())), tim.tolist()
 
 
-def stats_counters(delta, alg_bytes=0, violations=0, flagged=None):
-    """Counter dict from a stats delta (bench.stats_delta) and scan results."""
+def stats_counters(delta, alg_bytes=0, violations=0, flagged=None, **extra):
+    """Counter dict from a stats delta (bench.stats_delta), scan results and
+    extra integer counters (agree_compared, agree_missed, active)."""
     flagged = flagged or [0] * 8
     d = {"delivered_total": delta["delivered_total"], "commits": delta["commits"], "replies": delta["replies"],
          "dropped": delta["dropped"], "client_requests": delta["client_requests"], "alg_bytes": alg_bytes,
          "violations": violations}
+    d.update(extra)
     d.update({"flag_" + n: flagged[i] for i, n in enumerate(FLAG_NAMES)})
     return d

@@ -50,6 +50,20 @@ def load_library():
     L.paxisim_active_clusters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     L.paxisim_device_bytes.restype = C.c_int
     L.paxisim_device_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+    P = C.POINTER
+    L.paxisim_dist_init.restype = C.c_int
+    L.paxisim_dist_init.argtypes = [P(C.c_void_p), C.c_int, P(C.c_void_p)]
+    L.paxisim_dist_unique_id.restype = C.c_int
+    L.paxisim_dist_unique_id.argtypes = [C.c_char_p]
+    L.paxisim_dist_init_rank.restype = C.c_int
+    L.paxisim_dist_init_rank.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_int, P(C.c_void_p)]
+    L.paxisim_dist_allreduce.restype = C.c_int
+    L.paxisim_dist_allreduce.argtypes = [C.c_void_p, P(C.c_uint64), C.c_uint32, P(C.c_double), C.c_uint32,
+                                         P(C.c_uint64), P(C.c_double)]
+    L.paxisim_dist_stats.restype = C.c_int
+    L.paxisim_dist_stats.argtypes = [C.c_void_p, P(abi.Stats), P(C.c_double)]
+    L.paxisim_dist_destroy.restype = C.c_int
+    L.paxisim_dist_destroy.argtypes = [C.c_void_p]
     if L.paxisim_abi_version() != abi.ABI_VERSION:
         raise PaxisimError("ABI version mismatch between paxi_amd/abi.py and libpaxisim.so")
     _lib = L
@@ -60,7 +74,8 @@ EXPORTED = ["paxisim_abi_version", "paxisim_last_error", "paxisim_create", "paxi
             "paxisim_fault_add", "paxisim_step", "paxisim_sync", "paxisim_stats_get",
             "paxisim_read_state", "paxisim_read_instances", "paxisim_check", "paxisim_kernel_time", "paxisim_device_bytes",
             "paxisim_linearizable", "paxisim_history", "paxisim_occupancy", "paxisim_inject", "paxisim_read_log",
-            "paxisim_history_load", "paxisim_active_clusters"]
+            "paxisim_history_load", "paxisim_active_clusters", "paxisim_dist_init", "paxisim_dist_unique_id",
+            "paxisim_dist_init_rank", "paxisim_dist_allreduce", "paxisim_dist_stats", "paxisim_dist_destroy"]
 
 
 def _check(rc):
@@ -175,6 +190,61 @@ class Simulation:
 
     def __exit__(self, *a):
         self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Dist:
+    """RCCL reduction of statistics over handles (paxisim_dist_*): either one
+    process driving several handles (`Dist(sims)`) or one handle per process
+    (`Dist.join(sim, uid, nranks, rank)` with `uid` from `Dist.unique_id()` on
+    one rank, shipped by the caller's launcher)."""
+
+    def __init__(self, sims=None, _h=None, _members=1):
+        L = load_library()
+        self.h = C.c_void_p()
+        if _h is not None:
+            self.h, self.members = _h, _members
+            return
+        arr = (C.c_void_p * len(sims))(*[s.h.value for s in sims])
+        _check(L.paxisim_dist_init(arr, len(sims), C.byref(self.h)))
+        self.members = len(sims)
+
+    @staticmethod
+    def unique_id():
+        buf = C.create_string_buffer(128)
+        _check(load_library().paxisim_dist_unique_id(buf))
+        return buf.raw
+
+    @classmethod
+    def join(cls, sim, uid, nranks, rank):
+        h = C.c_void_p()
+        _check(load_library().paxisim_dist_init_rank(sim.h, uid, nranks, rank, C.byref(h)))
+        return cls(_h=h, _members=1)
+
+    def allreduce(self, sums, maxes):
+        """Sum `sums` (per member: a list of ints) and max `maxes` (per member: floats)."""
+        n, m = len(sums[0]) if sums else 0, len(maxes[0]) if maxes else 0
+        si = (C.c_uint64 * max(1, n * self.members))(*[int(v) for row in sums for v in row])
+        mi = (C.c_double * max(1, m * self.members))(*[float(v) for row in maxes for v in row])
+        so, mo = (C.c_uint64 * max(1, n))(), (C.c_double * max(1, m))()
+        _check(load_library().paxisim_dist_allreduce(self.h, si, n, mi, m, so, mo))
+        return list(so[:n]), list(mo[:m])
+
+    def stats(self):
+        """(paxisim_stats summed over the job, max step-kernel ms of any handle)"""
+        s, ms = abi.Stats(), C.c_double()
+        _check(load_library().paxisim_dist_stats(self.h, C.byref(s), C.byref(ms)))
+        return s, ms.value
+
+    def close(self):
+        if self.h:
+            load_library().paxisim_dist_destroy(self.h)
+            self.h = None
 
     def __del__(self):
         try:
