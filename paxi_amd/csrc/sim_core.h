@@ -356,6 +356,9 @@ __device__ __forceinline__ void fault_process(const Params& P, Rep<NT>& x, uint3
 #ifndef PXS_ABSORB_ABD
 #define PXS_ABSORB_ABD 0
 #endif
+#ifndef PXS_FLUSH_LATE
+#define PXS_FLUSH_LATE 1
+#endif
 
 // ---------------------------------------------------------------------------
 // One replica, one step
@@ -545,7 +548,9 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
     const unsigned long long q2 = stamp();
     st.disp += q2 - q1;
 #endif
+#if !PXS_FLUSH_LATE
     intent_flush<NT>(P, x);                             // one emit point for all lanes
+#endif
     if constexpr ((Proto::kind == PAXISIM_PAXOS && (PXS_ABSORB9 || NT != 9)) ||
                   (Proto::kind == PAXISIM_ABD && PXS_ABSORB_ABD)) {
       // Next messages whose handling is short and send-free (a P2b that does
@@ -568,6 +573,14 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
         }
       }
     }
+#if PXS_FLUSH_LATE
+    // The handler's pending send is emitted after the absorbed messages (they
+    // send nothing, so every link still sees its records in handler order):
+    // the record loads issued while absorbing then precede this flush's
+    // stores, and waiting for them does not wait for the stores (vmcnt
+    // retires loads and stores in issue order).
+    intent_flush<NT>(P, x);
+#endif
 #ifdef PXS_STAMPS
     fe = stamp();
     st.flush += fe - q2;

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Build a variant of libpaxisim.so with extra compile flags (A/B and diagnostics).
+# Usage: tools/build_variant.sh <out.so> [-DFLAG=V ...]     (run in this container, not on the GPU box)
+set -e -o pipefail
+OUT=$1; shift
+R=$(cd "$(dirname "$0")/.." && pwd)
+OBJ=$R/build/var_$(basename "$OUT" .so)
+mkdir -p "$OBJ" "$(dirname "$R/$OUT")"
+cd "$R"
+SRCS=$(python3 -c "import __graft_entry__ as g; print(' '.join(g.HIP_SOURCES))")
+pids=()
+for s in $SRCS; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c -o "$OBJ/${s%.hip}.o" "paxi_amd/csrc/$s" &
+  pids+=($!)
+done
+for p in "${pids[@]}"; do wait "$p"; done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$R/$OUT" "$OBJ"/*.o -ldl
+echo "built $OUT"

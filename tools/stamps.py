@@ -14,7 +14,7 @@ L.paxisim_step.argtypes = [C.c_void_p, C.c_uint32]
 L.paxisim_dbg_enable.argtypes = [C.c_void_p]
 L.paxisim_dbg_read.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
 clusters, warm, steps = (int(a) for a in sys.argv[1:4])
-cfg = abi.make_config(npz=[5], clusters=clusters, seed=42, window=16, mbox_cap=16, max_delay=4, steps_per_launch=50)
+cfg = abi.make_config(npz=[5], clusters=clusters, seed=42, window=16, mbox_cap=32, max_delay=4, steps_per_launch=50)
 wl = abi.make_workload(outstanding=8, target=0)
 fp = abi.make_fault_process(drop_ppm=1000, drop_len=50, slow_ppm=1000, slow_len=50, slow_min=1, slow_max=4)
 h = C.c_void_p()
