@@ -359,6 +359,9 @@ __device__ __forceinline__ void fault_process(const Params& P, Rep<NT>& x, uint3
 #ifndef PXS_FLUSH_LATE
 #define PXS_FLUSH_LATE 1
 #endif
+#ifndef PXS_PREFETCH2
+#define PXS_PREFETCH2 0   // 1: unstaged loop loads records two messages ahead (A/B r2l: -13% on config 2, more spills)
+#endif
 
 // ---------------------------------------------------------------------------
 // One replica, one step
@@ -500,6 +503,29 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
 #ifdef PXS_STAMPS
   st.stage += stamp() - g0;
 #endif
+  // PF2 (unstaged loop): records are loaded two messages ahead.  The pick
+  // after next assumes the next message is one record; a multi-record P1b
+  // invalidates it and it is picked again.  Picks draw statelessly, so a
+  // re-pick gives the same answer as the first pick of that index would.
+  constexpr bool PF2 = !STAGED && PXS_PREFETCH2;
+  auto pick_at = [&](uint32_t idx, uint32_t tot, uint32_t skip, uint32_t& psrc, uint32_t& pri) {
+    const uint32_t uu = draw(x.hs, tag(PUR_ORDER, x.r, idx >> 1));
+    uint32_t pk = (((idx & 1u) ? (uu >> 16) : (uu & 0xFFFFu)) * tot) >> 16;
+    bool found = false;
+    psrc = 0;
+    uint32_t p0 = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < NSMAX; s++) {
+      const uint32_t rs = opaque(rem[s]) - (s == skip ? 1u : 0u);
+      const bool here = !found && pk < rs;
+      if (here) { psrc = s; p0 = ((c0w[s >> 2] >> ((s & 3u) * 8u)) & 0xFFu) - rs; found = true; }
+      else if (!found) pk -= rs;
+    }
+    pri = (((box0 + psrc) * P.M + p0) << 6) | x.lane;
+  };
+  uint32_t nsrc = 0, nri = 0, q2s = 0, q2r = 0;
+  uint4 nm = make_uint4(0u, 0u, 0u, 0u), q2 = make_uint4(0u, 0u, 0u, 0u);
+  bool nv = false, q2v = false;                       // PF2: next / after-next pick loaded
   if (total) {
     pick(0, src, ri);
     if constexpr (STAGED) {
@@ -523,15 +549,30 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
     const unsigned long long q0 = stamp();
     st.wait += q0 - w0;               // trip head: message decode and FIFO bookkeeping
 #endif
-    uint32_t nsrc = 0, nri = 0;
-    uint4 nm = make_uint4(0u, 0u, 0u, 0u);
-    if (total) {
-      pick(i + 1u, nsrc, nri);
-      if constexpr (STAGED) {
-        if (i + 1u < jv) nm = stage[(i + 1u) * LANES];  // staged
-        else nm = load_now(x.rec + nri);                // past the stage: a blocking load
-      } else {
-        nm = x.rec[nri];                                // no stage: one message ahead from HBM
+    if constexpr (PF2) {
+      if (len > 1u) nv = false;                         // picked assuming a one-record message
+      if (!nv && total) {
+        pick_at(i + 1u, total, NSMAX, nsrc, nri);
+        nm = x.rec[nri];
+        nv = true;
+      }
+      q2v = nv && total > 1u;
+      if (q2v) {
+        pick_at(i + 2u, total - 1u, nsrc, q2s, q2r);
+        q2 = x.rec[q2r];
+      }
+    } else {
+      nsrc = 0;
+      nri = 0;
+      nm = make_uint4(0u, 0u, 0u, 0u);
+      if (total) {
+        pick(i + 1u, nsrc, nri);
+        if constexpr (STAGED) {
+          if (i + 1u < jv) nm = stage[(i + 1u) * LANES];  // staged
+          else nm = load_now(x.rec + nri);                // past the stage: a blocking load
+        } else {
+          nm = x.rec[nri];                                // no stage: one message ahead from HBM
+        }
       }
     }
 #ifdef PXS_STAMPS
@@ -545,8 +586,8 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
       Proto::template dispatch<NT>(P, x, src, m, ri);
     }
 #ifdef PXS_STAMPS
-    const unsigned long long q2 = stamp();
-    st.disp += q2 - q1;
+    const unsigned long long q2t = stamp();
+    st.disp += q2t - q1;
 #endif
 #if !PXS_FLUSH_LATE
     intent_flush<NT>(P, x);                             // one emit point for all lanes
@@ -566,7 +607,17 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
         for (uint32_t s = 0; s < NSMAX; s++) rem[s] = opaque(rem[s]) - (s == nsrc ? 1u : 0u);
         total -= 1u;
         i++;
-        if (total) {
+        if constexpr (PF2) {                            // the after-next becomes the next
+          nm = q2;
+          nsrc = q2s;
+          nri = q2r;
+          nv = q2v;
+          q2v = nv && total > 1u;
+          if (q2v) {
+            pick_at(i + 2u, total - 1u, nsrc, q2s, q2r);
+            q2 = x.rec[q2r];
+          }
+        } else if (total) {
           pick(i + 1u, nsrc, nri);
           if constexpr (STAGED) nm = i + 1u < jv ? stage[(i + 1u) * LANES] : load_now(x.rec + nri);
           else nm = x.rec[nri];
@@ -583,7 +634,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
 #endif
 #ifdef PXS_STAMPS
     fe = stamp();
-    st.flush += fe - q2;
+    st.flush += fe - q2t;
 #endif
 #ifdef PXS_STAMPS
     st.trips += 1;
@@ -591,6 +642,12 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
     src = nsrc;
     ri = nri;
     m = nm;
+    if constexpr (PF2) {
+      nm = q2;
+      nsrc = q2s;
+      nri = q2r;
+      nv = q2v;
+    }
     i++;
   }
 #pragma unroll
