@@ -59,7 +59,11 @@ extern "C" {
 enum paxisim_protocol {
   PAXISIM_PAXOS  = 0,   /* paxos/paxos.go + paxos/replica.go */
   PAXISIM_ABD    = 1,   /* abd/replica.go */
-  PAXISIM_WPAXOS = 2    /* wpaxos/replica.go + wpaxos/kpaxos.go */
+  PAXISIM_WPAXOS = 2,   /* wpaxos/replica.go + wpaxos/kpaxos.go */
+  PAXISIM_M2PAXOS = 3,  /* m2paxos/replica.go + m2paxos/kpaxos.go: WPaxos' per-key instances and
+                           leader stealing with Majority Q1/Q2, always adaptive */
+  PAXISIM_KPAXOS = 4    /* kpaxos/replica.go: per-key paxos.Paxos (Majority), static leader of a key
+                           by key range (index(), kpaxos/replica.go:32-44), no stealing */
 };
 
 /* ---- quorum predicates (quorum.go) ---- */
@@ -138,7 +142,7 @@ typedef struct paxisim_config {
   uint32_t window;            /* W: log window per replica (power of 2, 8..64) */
   uint32_t mbox_cap;          /* M: records per (link, arrival-step) bucket */
   uint32_t max_delay;         /* largest Slow delay in steps (<= PAXISIM_MAX_DELAY) */
-  uint32_t keys;              /* keys per cluster (ABD <= 64; WPaxos kpaxos instances <= 32) */
+  uint32_t keys;              /* keys per cluster (ABD <= 64; WPaxos/M2Paxos/KPaxos instances <= 32) */
   uint32_t steps_per_launch;  /* HIP backend: steps fused per kernel launch (0 = auto) */
   uint32_t history;           /* ABD: completed ops recorded per replica (0 = none) */
   int32_t  device;            /* HIP device ordinal */
@@ -178,6 +182,8 @@ typedef struct paxisim_workload {
   uint32_t start_step[PAXISIM_MAX_WORKERS]; /* step at which worker w's first request reaches
                                  target[w] (0 = at creation): e.g. clients that turn to
                                  another replica after a crash (BASELINE config 4) */
+  uint32_t key_min;           /* Bconfig.Min (benchmark.go:34): the key value of key index 0; only
+                                 KPaxos' static leader assignment reads key values */
 } paxisim_workload;
 
 /* Random fault process, applied per (cluster, src, dst) link every step. */

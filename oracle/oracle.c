@@ -230,6 +230,8 @@ struct oracle_sim {
   uint32_t NK;                     /* Paxos instances per replica: WPaxos keys, else 1 */
   uint32_t q1, q2;                 /* quorum kinds in use (WPaxos: from fz, wpaxos/kpaxos.go:16-28) */
   uint32_t late_workers;           /* some worker has start_step > 0 */
+  uint32_t variant;                /* per-key protocol (cfg.protocol reads WPAXOS): WPAXOS, M2PAXOS, KPAXOS */
+  uint32_t zfirst[PAXISIM_MAX_ZONES]; /* replica index of "z.1" */
   uint32_t AR;                     /* agreement ring: checkpoints kept per (cluster, instance) */
 };
 
@@ -911,9 +913,23 @@ static uint32_t policy_hit(ctx_t* x, uint32_t id) {
   return res;
 }
 
+/* KPaxos index() (kpaxos/replica.go:32-44): leader "z.1", z = 1 + key/200 (at
+ * most 5); an ID outside the configuration is an unknown address. */
+static uint32_t kp_leader(const struct oracle_sim* s, uint32_t key) {
+  const uint32_t z = key < 800u ? key / 200u : 4u;
+  return z < s->Z ? s->zfirst[z] : NO_ID;
+}
+
 static void wp_handle_request(ctx_t* x, uint32_t req) {   /* replica.go:42-66 */
   const struct oracle_sim* s = x->s;
-  wp_init(x, wl_key(s, x->c->kc, REQ_CID(req)));
+  const uint32_t key = wl_key(s, x->c->kc, REQ_CID(req));
+  wp_init(x, key);
+  if (s->variant == PAXISIM_KPAXOS) {                      /* kpaxos/replica.go:52-62 */
+    const uint32_t leader = kp_leader(s, s->wl.key_min + key);
+    if (leader == x->r) paxos_handle_request(x, req);
+    else node_forward(x, leader, req);                     /* `go r.Forward(leader, m)` */
+    return;
+  }
   if (!s->cfg.adaptive) {
     paxos_handle_request(x, req);
     return;
@@ -1264,7 +1280,15 @@ int oracle_create(const paxisim_config* cfg, const paxisim_workload* wl,
   uint64_t i;
   paxisim_fault_process nofp;
   int rc;
+  paxisim_config ncfg;
+  uint32_t variant;
   if (!cfg || !wl || !out) return fail(PAXISIM_EINVAL, "null argument");
+  /* M2Paxos and KPaxos are per-key Paxos as WPaxos is: same state, another
+   * request path and Majority quorums (m2paxos/kpaxos.go:15-21, kpaxos/replica.go) */
+  ncfg = *cfg;
+  variant = cfg->protocol;
+  if (variant == PAXISIM_M2PAXOS || variant == PAXISIM_KPAXOS) ncfg.protocol = PAXISIM_WPAXOS;
+  cfg = &ncfg;
   if (!fp) { memset(&nofp, 0, sizeof nofp); fp = &nofp; }
   if ((rc = check_config(cfg, wl, fp, &N))) return rc;
   s = (struct oracle_sim*)calloc(1, sizeof *s);
@@ -1295,6 +1319,10 @@ int oracle_create(const paxisim_config* cfg, const paxisim_workload* wl,
     s->cfg.reply_when_commit = 0;
     s->cfg.ephemeral_leader = 0;
   }
+  s->variant = variant;
+  if (variant == PAXISIM_M2PAXOS || variant == PAXISIM_KPAXOS) s->q1 = s->q2 = PAXISIM_Q_MAJORITY;
+  if (variant == PAXISIM_M2PAXOS) s->cfg.adaptive = 1;      /* m2paxos/replica.go:34-52: no -adaptive switch */
+  for (z = 0, r = 0; z < s->Z; r += cfg->npz[z], z++) s->zfirst[z] = r;
   s->cl = (cluster_t*)calloc(s->C, sizeof(cluster_t));
   if (!s->cl) { free(s); return fail(PAXISIM_ENOMEM, "oom clusters"); }
   for (i = 0; i < s->C; i++) {

@@ -22,7 +22,8 @@ ALL_DST = 0xFF
 OK, EINVAL, ENOMEM, EDEVICE, EUNSUPP, ERANGE = 0, -1, -2, -3, -4, -5
 
 # protocols (server/server.go:38-84)
-PAXOS, ABD, WPAXOS = 0, 1, 2
+PAXOS, ABD, WPAXOS, M2PAXOS, KPAXOS = 0, 1, 2, 3, 4
+PER_KEY = (WPAXOS, M2PAXOS, KPAXOS)   # protocols with one Paxos instance per key
 
 # quorum predicates (quorum.go)
 Q_MAJORITY, Q_ALL, Q_FAST, Q_GRID_ROW, Q_ZONE_MAJORITY, Q_GRID_COLUMN, Q_FGRID_Q1, Q_FGRID_Q2 = range(8)
@@ -90,6 +91,7 @@ class Workload(C.Structure):
         ("conflicts", C.c_uint32),
         ("key_cdf", C.c_uint32 * MAX_KEYS),
         ("start_step", C.c_uint32 * MAX_WORKERS),
+        ("key_min", C.c_uint32),
     ]
 
 
@@ -227,13 +229,14 @@ def make_config(npz=(5,), protocol=PAXOS, q1=Q_MAJORITY, q2=Q_MAJORITY, fz=0, th
 
 
 def make_workload(outstanding=1, max_requests=0, write_ppm=1_000_000, locality_ppm=0, target=0,
-                  distribution="uniform", keys=None, start_step=0, **dist_params):
+                  distribution="uniform", keys=None, start_step=0, key_min=0, **dist_params):
     """Closed-loop workload.  `distribution` is a Bconfig.Distribution name
     (benchmark.go:202-233, see paxi_amd.workload); the table distributions
     ("normal", "zipfan", "exponential") need the cluster's `keys`."""
     from . import workload as _wl
     w = Workload()
     w.outstanding, w.max_requests, w.write_ppm, w.locality_ppm = outstanding, max_requests, write_ppm, locality_ppm
+    w.key_min = key_min
     for i in range(MAX_WORKERS):
         w.target[i] = target[i % len(target)] if isinstance(target, (list, tuple)) else target
         w.start_step[i] = start_step[i % len(start_step)] if isinstance(start_step, (list, tuple)) else start_step
@@ -262,4 +265,4 @@ def n_replicas(cfg):
 
 def n_instances(cfg):
     """Paxos instances per replica: one kpaxos per key for WPaxos, else one."""
-    return cfg.keys if cfg.protocol == WPAXOS else 1
+    return cfg.keys if cfg.protocol in PER_KEY else 1

@@ -655,6 +655,12 @@ static StepOps step_ops_for(uint32_t protocol, uint32_t N) {
 extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload* wl, const paxisim_fault_process* fp,
                               paxisim** out) {
   if (!cfg || !wl || !out) return fail(PAXISIM_EINVAL, "null argument");
+  // M2Paxos and KPaxos are per-key Paxos like WPaxos: same kernel and state, a
+  // different request path and quorums (P.variant)
+  paxisim_config ncfg = *cfg;
+  const uint32_t variant = cfg->protocol;
+  if (variant == PAXISIM_M2PAXOS || variant == PAXISIM_KPAXOS) ncfg.protocol = PAXISIM_WPAXOS;
+  cfg = &ncfg;
   paxisim_fault_process nofp;
   memset(&nofp, 0, sizeof nofp);
   if (!fp) fp = &nofp;
@@ -722,6 +728,13 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     P.rwc = 0;
     P.ephemeral = 0;
   }
+  P.variant = cfg->protocol == PAXISIM_WPAXOS ? variant : cfg->protocol;
+  if (P.variant == PAXISIM_M2PAXOS || P.variant == PAXISIM_KPAXOS) {   // m2paxos/kpaxos.go:15-21; paxos.NewPaxos default
+    P.q1 = PAXISIM_Q_MAJORITY;
+    P.q2 = PAXISIM_Q_MAJORITY;
+  }
+  if (P.variant == PAXISIM_M2PAXOS) P.adaptive = 1;
+  P.key_min = wl->key_min;   // m2paxos/replica.go:34-52 has no -adaptive switch
   P.max_delay = cfg->max_delay;
   P.drop_ppm = fp->drop_ppm;
   P.drop_len = fp->drop_len;
@@ -738,6 +751,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
       h->zone_of[r] = z + 1;
       h->node_of[r] = k + 1;
     }
+    P.zfirst[z] = r - cfg->npz[z];
   }
   for (uint32_t w = 0; w < PAXISIM_MAX_WORKERS; w++) {
     P.target[w] = wl->target[w];

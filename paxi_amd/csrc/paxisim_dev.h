@@ -140,6 +140,9 @@ struct Params {
   uint32_t* qf;          // [C] per slot
   uint32_t* bound;       // device scalar: slots [0, *bound) are stepped
   uint32_t compact;      // protocol supports compaction and it is enabled
+  uint32_t variant;      // per-key protocol run by the WPaxos kernel: WPAXOS, M2PAXOS or KPAXOS
+  uint32_t zfirst[PAXISIM_MAX_ZONES];   // replica index of "z.1" (KPaxos static leaders)
+  uint32_t key_min;      // Bconfig.Min: key value of key index 0
 };
 
 // slot of local cluster c

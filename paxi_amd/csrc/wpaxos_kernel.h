@@ -177,9 +177,24 @@ __device__ __forceinline__ uint32_t policy_hit(const Params& P, Rep<NT>& x, uint
   return res;
 }
 
+// KPaxos index() (kpaxos/replica.go:32-44): the static leader of a key is
+// "z.1" with z = 1 + key / 200 (at most 5); an ID that is not in the
+// configuration is an unknown address, whose sends are dropped (socket.go:86-88).
+template <int NT>
+__device__ __forceinline__ uint32_t kp_leader(const Params& P, uint32_t key) {
+  const uint32_t z = key < 800u ? key / 200u : 4u;
+  return z < P.Z ? P.zfirst[z] : NO_ID;
+}
+
 template <int NT>
 __device__ __forceinline__ void wp_handle_request(const Params& P, Rep<NT>& x, uint32_t req) {  // replica.go:42-66
   wp_create<NT>(P, x);                                                 // r.init(key)
+  if (P.variant == PAXISIM_KPAXOS) {                                   // kpaxos/replica.go:52-62
+    const uint32_t leader = kp_leader<NT>(P, P.key_min + x.key);
+    if (leader == x.r) paxos_handle_request<NT>(P, x, req);
+    else node_forward<NT>(P, x, leader, req);                          // `go r.Forward(leader, m)`
+    return;
+  }
   if (!P.adaptive) {
     paxos_handle_request<NT>(P, x, req);
     return;
