@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PAXISIM_ABI_VERSION 8
+#define PAXISIM_ABI_VERSION 9
 
 #define PAXISIM_MAX_N        16  /* replicas per cluster (ack masks are u16) */
 #define PAXISIM_MAX_ZONES    16
@@ -62,8 +62,11 @@ enum paxisim_protocol {
   PAXISIM_WPAXOS = 2,   /* wpaxos/replica.go + wpaxos/kpaxos.go */
   PAXISIM_M2PAXOS = 3,  /* m2paxos/replica.go + m2paxos/kpaxos.go: WPaxos' per-key instances and
                            leader stealing with Majority Q1/Q2, always adaptive */
-  PAXISIM_KPAXOS = 4    /* kpaxos/replica.go: per-key paxos.Paxos (Majority), static leader of a key
+  PAXISIM_KPAXOS = 4,   /* kpaxos/replica.go: per-key paxos.Paxos (Majority), static leader of a key
                            by key range (index(), kpaxos/replica.go:32-44), no stealing */
+  PAXISIM_EPAXOS = 5    /* epaxos/replica.go, instance.go: leaderless; every replica leads its own
+                           instances (PreAccept fast path on FastQuorum, quorum.go:65-67, else
+                           Accept on Majority); execution walks each owner's log in slot order */
 };
 
 /* ---- quorum predicates (quorum.go) ---- */
@@ -94,7 +97,12 @@ enum paxisim_msg {
   PAXISIM_MSG_SET       = 11, /* abd/msg.go:33-39 */
   PAXISIM_MSG_SETREPLY  = 12, /* abd/msg.go:42-46 */
   PAXISIM_MSG_LEADERCHG = 13, /* wpaxos/msg.go:78-84 */
-  PAXISIM_NMSG          = 16
+  PAXISIM_MSG_PREACCEPT = 14, /* epaxos/msg.go:18-25 (payload: seq, Dep) */
+  PAXISIM_MSG_PREACCEPTREPLY = 15, /* epaxos/msg.go:31-38 (payload: Dep, Committed) */
+  PAXISIM_MSG_ACCEPT    = 16, /* epaxos/msg.go:44-50 (payload: Dep) */
+  PAXISIM_MSG_ACCEPTREPLY = 17, /* epaxos/msg.go:52-56 */
+  PAXISIM_MSG_COMMIT    = 18, /* epaxos/msg.go:58-65 (payload: seq, Dep) */
+  PAXISIM_NMSG          = 20
 };
 
 /* ---- per-replica / per-cluster flags ---- */

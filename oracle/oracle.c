@@ -128,6 +128,11 @@ typedef struct { uint32_t slot, ballot, commit, until; } ghost_t;
 #define HDR_TYPE(h) ((h) & 0xFFu)
 #define HDR_N(h) (((h) >> 8) & 0xFFu)
 #define HDR_KEY(h) ((h) >> 16)       /* WPaxos key (wpaxos/msg.go Key fields) */
+/* records of a message: a P1b and the EPaxos messages carry payload records */
+static inline uint32_t rec_len(uint32_t h) {
+  const uint32_t t = HDR_TYPE(h);
+  return 1u + ((t == PAXISIM_MSG_P1B || (t >= PAXISIM_MSG_PREACCEPT && t <= PAXISIM_MSG_COMMIT)) ? HDR_N(h) : 0u);
+}
 
 /* log entry (paxos/paxos.go:11-18): ballot, command, request, quorum, commit */
 typedef struct { uint32_t ballot, cmd, req, meta; } entry_t;
@@ -183,8 +188,23 @@ typedef struct inst {
   ghost_t ghost[GMAX];
 } inst_t;
 
+/* EPaxos instance (epaxos/instance.go:16-28); dep[id] = 0 reads as absent, as a Go map does */
+typedef struct {
+  uint32_t cmd, req, acks;
+  int32_t seq, slot;               /* slot: which of the ring's slots this entry holds */
+  uint8_t exists, ballot, status, changed;
+  uint32_t nrep;                   /* replies sent for this instance's request */
+  int32_t dep[PAXISIM_MAX_N];
+} ep_inst_t;
+
 typedef struct replica {
   inst_t* inst;                    /* NK instances (key-major) */
+  /* EPaxos (epaxos/replica.go:14-27): per owner log ring, slot/committed/executed, conflicts */
+  ep_inst_t* ep_log;               /* [N][W] */
+  int32_t ep_slot[PAXISIM_MAX_N], ep_committed[PAXISIM_MAX_N], ep_executed[PAXISIM_MAX_N];
+  int32_t* ep_cf;                  /* [N][keys][2] {slot or -1, seq} */
+  int32_t* ep_maxseq;              /* [keys], -1 = absent */
+  uint32_t ep_execs;               /* Execute calls (re-executions included) */
   /* node.forwards (node.go:35, 165-172) */
   uint32_t nfwd, fwd[FMAX];
   /* socket fault state (socket.go:26-34), random process */
@@ -972,6 +992,324 @@ static void wpaxos_dispatch(ctx_t* x, uint32_t src, const rec_t* m) {   /* regis
 }
 
 /* ------------------------------------------------------------------------ */
+/* EPaxos (epaxos/replica.go, epaxos/instance.go)                            */
+/* Leaderless: a replica leads the instances of its own log.  Instance (o, s)*/
+/* of owner o lives in a ring of W over slots (executed[o], executed[o] + W];*/
+/* slots at or below executed[o] are COMMITTED for good (execute() only      */
+/* advances over committed instances, and no handler changes one after it);  */
+/* a message for a slot beyond the ring cannot be held: WOVF | UNFAITHFUL.   */
+/* Records: PreAccept {hdr, ballot, slot, cmd} + (seq, Dep[N]);              */
+/* PreAcceptReply {hdr, ballot, slot, seq} + (Dep[N], Committed[N]);        */
+/* Accept {hdr, ballot, slot, seq} + Dep[N]; AcceptReply {hdr, ballot, slot};*/
+/* Commit {hdr, ballot, slot, cmd} + (seq, Dep[N]).  The owner of an        */
+/* instance is the sender of PreAccept/Accept/Commit (only it sends them).  */
+/* Ballots are NewBallot(0, owner) only (replica.go:77): stored as 1 + owner.*/
+/* ------------------------------------------------------------------------ */
+enum { EP_NONE = 0, EP_PREACCEPTED = 1, EP_ACCEPTED = 2, EP_COMMITTED = 3 };
+
+static inline uint32_t ep_words_rec(uint32_t words) { return (words + 3u) / 4u; }
+static ep_inst_t* ep_ring(ctx_t* x, uint32_t o, int32_t s) {
+  return &x->n->ep_log[(size_t)o * x->s->W + ((uint32_t)s & (x->s->W - 1u))];
+}
+/* the ring entry holds instance s (an entry keeps its data after execute()
+ * passes it, as Go keeps the instance, until a later slot takes the entry) */
+static inline int ep_live(const ep_inst_t* i, int32_t s) { return i->exists && i->slot == s; }
+static inline void ep_new(ep_inst_t* i, int32_t s) { memset(i, 0, sizeof *i); i->exists = 1; i->slot = s; }
+/* 1: in the ring (*out), 0: at or below executed (COMMITTED), 2: beyond the ring */
+static int ep_where(ctx_t* x, uint32_t o, int32_t s, ep_inst_t** out) {
+  const int32_t ex = x->n->ep_executed[o];
+  if (s <= ex) return 0;
+  if (s > ex + (int32_t)x->s->W) return 2;
+  *out = ep_ring(x, o, s);
+  return 1;
+}
+static inline int32_t* ep_cf(ctx_t* x, uint32_t o, uint32_t key) {       /* {slot (-1 none), seq} */
+  return &x->n->ep_cf[((size_t)o * x->s->cfg.keys + key) * 2u];
+}
+static inline uint32_t ep_key(ctx_t* x, uint32_t cmd) { return wl_key(x->s, x->c->kc, cmd); }
+
+/* the current seq of instance (o, d), the slot conflicts[o][key] names */
+static int32_t ep_seq_of(ctx_t* x, uint32_t o, int32_t d, uint32_t key) {
+  ep_inst_t* i;
+  if (ep_where(x, o, d, &i) == 1 && ep_live(i, d)) return i->seq;
+  return ep_cf(x, o, key)[1];                              /* left the ring with this seq */
+}
+
+/* attributes (replica.go:58-80) */
+static void ep_attributes(ctx_t* x, uint32_t key, int32_t* seq_out, int32_t* dep) {
+  const struct oracle_sim* s = x->s;
+  int32_t seq = 0;
+  uint32_t id;
+  for (id = 0; id < s->N; id++) dep[id] = 0;
+  for (id = 0; id < s->N; id++) {                          /* Go ranges over a map: max, order-free */
+    const int32_t* cf = ep_cf(x, id, key);
+    if (cf[0] >= 0 && cf[0] > dep[id]) {
+      const int32_t sd = ep_seq_of(x, id, cf[0], key);
+      dep[id] = cf[0];
+      if (seq <= sd) seq = sd + 1;
+    }
+  }
+  if (x->n->ep_maxseq[key] >= 0 && seq <= x->n->ep_maxseq[key]) seq = x->n->ep_maxseq[key] + 1;
+  *seq_out = seq;
+}
+
+/* update (replica.go:83-101) */
+static void ep_update(ctx_t* x, uint32_t cmd, uint32_t id, int32_t slot, int32_t seq) {
+  const uint32_t k = ep_key(x, cmd);
+  int32_t* cf = ep_cf(x, id, k);
+  if (cf[0] < 0 || cf[0] < slot) { cf[0] = slot; cf[1] = seq; }
+  if (x->n->ep_maxseq[k] < seq) x->n->ep_maxseq[k] = seq;    /* -1 = absent */
+}
+
+static void ep_send(ctx_t* x, uint32_t to, uint32_t type, uint32_t w1, uint32_t w2, uint32_t w3,
+                    const uint32_t* pay, uint32_t npay) {
+  rec_t m[1 + (2 * PAXISIM_MAX_N + 3) / 4];
+  const uint32_t n = ep_words_rec(npay);
+  uint32_t k;
+  memset(m, 0, sizeof m);
+  m[0].hdr = HDR(type, n); m[0].ballot = w1; m[0].slot = w2; m[0].cid = w3;
+  for (k = 0; k < npay; k++) ((uint32_t*)&m[1])[k] = pay[k];
+  sock_send(x, to, m, 1u + n);
+}
+static void ep_broadcast(ctx_t* x, uint32_t type, uint32_t w1, uint32_t w2, uint32_t w3, const uint32_t* pay,
+                         uint32_t npay) {
+  uint32_t d;
+  for (d = 0; d < x->s->N; d++)
+    if (d != x->r) ep_send(x, d, type, w1, w2, w3, pay, npay);
+}
+
+static void ep_reply(ctx_t* x, ep_inst_t* i) {           /* i.request.Reply (message.go:32-34) */
+  /* req.c is buffered 1 (http.go:97): the HTTP handler takes the first reply,
+   * the second waits in the buffer, a third would block this goroutine */
+  if (++i->nrep >= 3) raise_flag(x, PAXISIM_F_UNFAITHFUL);
+  request_reply(x, i->req, i->cmd);
+}
+
+/* execute (replica.go:355-384): owners in index order where Go ranges over a map */
+static void ep_execute(ctx_t* x) {
+  const struct oracle_sim* s = x->s;
+  replica_t* p = x->n;
+  uint32_t id;
+  for (id = 0; id < s->N; id++) {
+    int32_t sl;
+    for (sl = p->ep_executed[id] + 1; sl <= p->ep_slot[id]; sl++) {
+      ep_inst_t* i = NULL;
+      const int w = ep_where(x, id, sl, &i);
+      if (w == 2) { raise_flag(x, PAXISIM_F_WOVF | PAXISIM_F_UNFAITHFUL); continue; }
+      if (!ep_live(i, sl)) continue;                       /* nil: skipped, not executed */
+      if (i->status != EP_COMMITTED) break;
+      p->inst[0].digest = mix64(p->inst[0].digest ^ (((uint64_t)((id << 24) | (uint32_t)sl) << 32) | i->cmd));
+      p->ep_execs++;
+      if (s->keep_xlog) {
+        inst_t* q = &p->inst[0];
+        if (q->nx == q->capx) {
+          q->capx = q->capx ? 2 * q->capx : 1024;
+          q->xlog = (uint32_t*)realloc(q->xlog, q->capx * sizeof(uint32_t));
+        }
+        q->xlog[q->nx++] = i->cmd;
+      }
+      if (i->req) ep_reply(x, i);
+      if (sl == p->ep_executed[id] + 1) {
+        const uint32_t k = ep_key(x, i->cmd);
+        int32_t* cf = ep_cf(x, id, k);
+        if (cf[0] == sl) cf[1] = i->seq;                   /* it leaves the ring with this seq */
+        p->ep_executed[id] = sl;
+      }
+    }
+  }
+}
+
+/* updateCommit (replica.go:103-111) */
+static void ep_update_commit(ctx_t* x, uint32_t id) {
+  replica_t* p = x->n;
+  for (;;) {
+    ep_inst_t* i = NULL;
+    const int32_t nx = p->ep_committed[id] + 1;
+    const int w = ep_where(x, id, nx, &i);
+    if (w == 2) {
+      if (nx <= p->ep_slot[id]) raise_flag(x, PAXISIM_F_WOVF | PAXISIM_F_UNFAITHFUL);
+      break;
+    }
+    if (w == 1 && !(ep_live(i, nx) && i->status == EP_COMMITTED)) break;
+    p->ep_committed[id] = nx;                              /* w == 0: committed for good */
+  }
+  ep_execute(x);
+}
+
+static void ep_handle_request(ctx_t* x, uint32_t req) {    /* replica.go:113-145 */
+  replica_t* p = x->n;
+  const uint32_t self = x->r, cmd = REQ_CID(req), key = ep_key(x, cmd);
+  int32_t seq, dep[PAXISIM_MAX_N], s;
+  ep_inst_t* i = NULL;
+  uint32_t pay[1 + PAXISIM_MAX_N], k;
+  p->ep_slot[self]++;
+  s = p->ep_slot[self];
+  ep_attributes(x, key, &seq, dep);
+  if (ep_where(x, self, s, &i) != 1) { raise_flag(x, PAXISIM_F_WOVF | PAXISIM_F_UNFAITHFUL); return; }
+  ep_new(i, s);
+  i->cmd = cmd; i->ballot = (uint8_t)(1u + self); i->status = EP_PREACCEPTED;
+  i->seq = seq; memcpy(i->dep, dep, sizeof dep); i->req = req;
+  i->acks = 1u << self;                                    /* self ack */
+  ep_update(x, cmd, self, s, seq);
+  pay[0] = (uint32_t)seq;
+  for (k = 0; k < x->s->N; k++) pay[1 + k] = (uint32_t)dep[k];
+  ep_broadcast(x, PAXISIM_MSG_PREACCEPT, i->ballot, (uint32_t)s, cmd, pay, 1u + x->s->N);
+}
+
+static void ep_handle_preaccept(ctx_t* x, uint32_t o, const rec_t* m) {   /* replica.go:147-191 */
+  replica_t* p = x->n;
+  const uint32_t* pw = (const uint32_t*)(m + 1);
+  const int32_t s = (int32_t)m->slot;
+  const uint32_t mb = m->ballot, mcmd = m->cid;
+  int32_t seq, dep[PAXISIM_MAX_N];
+  ep_inst_t* i = NULL;
+  uint32_t pay[2 * PAXISIM_MAX_N], k;
+  const int w = ep_where(x, o, s, &i);
+  if (w == 0) return;                                      /* COMMITTED, cmd set: no reply */
+  if (w == 2) { raise_flag(x, PAXISIM_F_WOVF | PAXISIM_F_UNFAITHFUL); return; }
+  if (!ep_live(i, s)) ep_new(i, s);                         /* &instance{} */
+  if (i->status == EP_COMMITTED || i->status == EP_ACCEPTED) {
+    if (!i->cmd) { i->cmd = mcmd; ep_update(x, mcmd, o, s, (int32_t)pw[0]); }
+    return;
+  }
+  if (s > p->ep_slot[o]) p->ep_slot[o] = s;
+  ep_attributes(x, ep_key(x, mcmd), &seq, dep);
+  if (mb >= i->ballot) {
+    i->ballot = (uint8_t)mb; i->cmd = mcmd; i->status = EP_PREACCEPTED; i->seq = seq;
+    memcpy(i->dep, dep, sizeof dep);
+  }
+  ep_update(x, mcmd, o, s, seq);
+  for (k = 0; k < x->s->N; k++) {
+    pay[k] = (uint32_t)i->dep[k];
+    pay[x->s->N + k] = (uint32_t)p->ep_committed[k];
+  }
+  ep_send(x, o, PAXISIM_MSG_PREACCEPTREPLY, i->ballot, (uint32_t)s, (uint32_t)seq, pay, 2u * x->s->N);
+}
+
+static void ep_commit_broadcast(ctx_t* x, ep_inst_t* i, int32_t s) {
+  uint32_t pay[1 + PAXISIM_MAX_N], k;
+  pay[0] = (uint32_t)i->seq;
+  for (k = 0; k < x->s->N; k++) pay[1 + k] = (uint32_t)i->dep[k];
+  ep_broadcast(x, PAXISIM_MSG_COMMIT, i->ballot, (uint32_t)s, i->cmd, pay, 1u + x->s->N);
+}
+
+static void ep_handle_preaccept_reply(ctx_t* x, uint32_t src, const rec_t* m) {   /* replica.go:193-260 */
+  const struct oracle_sim* s = x->s;
+  replica_t* p = x->n;
+  const uint32_t* pw = (const uint32_t*)(m + 1);
+  const int32_t sl = (int32_t)m->slot;
+  ep_inst_t* i = NULL;
+  int committed = 1;
+  uint32_t id;
+  if (ep_where(x, x->r, sl, &i) != 1 || !ep_live(i, sl)) return;   /* executed: COMMITTED */
+  if (i->status != EP_PREACCEPTED) return;
+  if (m->ballot > i->ballot) return;
+  i->acks |= 1u << src;
+  if ((int32_t)m->cid > i->seq) { i->seq = (int32_t)m->cid; i->changed = 1; }     /* merge (instance.go:30-41) */
+  for (id = 0; id < s->N; id++)
+    if ((int32_t)pw[id] > i->dep[id]) { i->dep[id] = (int32_t)pw[id]; i->changed = 1; }
+  for (id = 0; id < s->N; id++) {
+    const int32_t d = (int32_t)pw[s->N + id];
+    if (d > p->ep_committed[id]) p->ep_committed[id] = d;
+    if (p->ep_committed[id] >= 0 && p->ep_committed[id] < i->dep[id]) committed = 0;
+  }
+  if (popc(i->acks) >= (int)(s->N * 3 / 4)) {             /* FastQuorum (quorum.go:65-67) */
+    if (!i->changed && committed) {                        /* fast path */
+      i->status = EP_COMMITTED;
+      p->commits++;
+      ep_update_commit(x, x->r);
+      ep_commit_broadcast(x, i, sl);
+      if (s->cfg.reply_when_commit && i->req) ep_reply(x, i);
+    } else {                                               /* slow path */
+      uint32_t pay[PAXISIM_MAX_N], k;
+      i->status = EP_ACCEPTED;
+      i->acks = 1u << x->r;
+      for (k = 0; k < s->N; k++) pay[k] = (uint32_t)i->dep[k];
+      ep_broadcast(x, PAXISIM_MSG_ACCEPT, i->ballot, (uint32_t)sl, (uint32_t)i->seq, pay, s->N);
+    }
+  }
+}
+
+static void ep_handle_accept(ctx_t* x, uint32_t o, const rec_t* m) {   /* replica.go:262-290 */
+  replica_t* p = x->n;
+  const uint32_t* pw = (const uint32_t*)(m + 1);
+  const int32_t s = (int32_t)m->slot;
+  ep_inst_t* i = NULL;
+  uint32_t k;
+  const int w = ep_where(x, o, s, &i);
+  if (w == 0) return;
+  if (w == 2) { raise_flag(x, PAXISIM_F_WOVF | PAXISIM_F_UNFAITHFUL); return; }
+  if (!ep_live(i, s)) ep_new(i, s);
+  if (i->status == EP_COMMITTED) return;
+  if (s > p->ep_slot[o]) p->ep_slot[o] = s;
+  if (m->ballot >= i->ballot) {
+    i->status = EP_ACCEPTED; i->ballot = (uint8_t)m->ballot; i->seq = (int32_t)m->cid;
+    for (k = 0; k < x->s->N; k++) i->dep[k] = (int32_t)pw[k];
+  }
+  send1(x, o, PAXISIM_MSG_ACCEPTREPLY, i->ballot, (uint32_t)s, 0);
+}
+
+static void ep_handle_accept_reply(ctx_t* x, uint32_t src, const rec_t* m) {   /* replica.go:292-321 */
+  const int32_t sl = (int32_t)m->slot;
+  ep_inst_t* i = NULL;
+  if (ep_where(x, x->r, sl, &i) != 1 || !ep_live(i, sl)) return;
+  if (i->status != EP_ACCEPTED) return;
+  if (i->ballot < m->ballot) { i->ballot = (uint8_t)m->ballot; return; }
+  i->acks |= 1u << src;
+  if (popc(i->acks) > (int)(x->s->N / 2)) {              /* Majority */
+    i->status = EP_COMMITTED;
+    x->n->commits++;
+    ep_update_commit(x, x->r);
+    if (x->s->cfg.reply_when_commit && i->req) ep_reply(x, i);
+    ep_commit_broadcast(x, i, sl);
+  }
+}
+
+static void ep_handle_commit(ctx_t* x, uint32_t o, const rec_t* m) {   /* replica.go:323-353 */
+  replica_t* p = x->n;
+  const uint32_t* pw = (const uint32_t*)(m + 1);
+  const int32_t s = (int32_t)m->slot;
+  ep_inst_t* i = NULL;
+  uint32_t k;
+  const int w = ep_where(x, o, s, &i);
+  if (s > p->ep_slot[o]) p->ep_slot[o] = s;
+  if (w == 2) { raise_flag(x, PAXISIM_F_WOVF | PAXISIM_F_UNFAITHFUL); return; }
+  if (w == 0) {                                            /* committed for good: re-commit in place */
+    int32_t* cf = ep_cf(x, o, ep_key(x, m->cid));
+    ep_update(x, m->cid, o, s, (int32_t)pw[0]);
+    if (cf[0] == s) cf[1] = (int32_t)pw[0];
+    ep_update_commit(x, o);
+    return;
+  }
+  if (!ep_live(i, s)) ep_new(i, s);
+  if (m->ballot >= i->ballot) {
+    i->ballot = (uint8_t)m->ballot; i->cmd = m->cid; i->status = EP_COMMITTED; i->seq = (int32_t)pw[0];
+    for (k = 0; k < x->s->N; k++) i->dep[k] = (int32_t)pw[1 + k];
+    ep_update(x, m->cid, o, s, (int32_t)pw[0]);
+  }
+  if (i->req) {                                            /* r.Retry: back into MessageChan */
+    client_enqueue(x, x->r, REQ_CID(i->req));
+    i->req = 0;
+  }
+  ep_update_commit(x, o);
+}
+
+static void epaxos_dispatch(ctx_t* x, uint32_t src, const rec_t* m) {   /* registrations replica.go:49-54 */
+  switch (HDR_TYPE(m->hdr)) {
+    case PAXISIM_MSG_REQUEST:
+      ep_handle_request(x, REQ(m->cid, src == x->s->N ? PAXISIM_CLIENT_SRC : src));
+      break;
+    case PAXISIM_MSG_REPLY: handle_reply(x, m->cid); break;
+    case PAXISIM_MSG_PREACCEPT: ep_handle_preaccept(x, src, m); break;
+    case PAXISIM_MSG_PREACCEPTREPLY: ep_handle_preaccept_reply(x, src, m); break;
+    case PAXISIM_MSG_ACCEPT: ep_handle_accept(x, src, m); break;
+    case PAXISIM_MSG_ACCEPTREPLY: ep_handle_accept_reply(x, src, m); break;
+    case PAXISIM_MSG_COMMIT: ep_handle_commit(x, src, m); break;
+    default: break;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
 /* ABD atomic storage (abd/replica.go)                                       */
 /* Record fields: hdr = type | key << 8, ballot = coordinator op id (CID),   */
 /* slot = version, cid = value (a write's value is its command id; 0 = nil). */
@@ -1153,7 +1491,7 @@ static void replica_step(const struct oracle_sim* s, cluster_t* c, uint32_t r, u
       while (k < rem[src]) {
         rec_t* m = mb_rec(s, c, b, r, src, k);
         x.n->discarded++;
-        k += 1u + (HDR_TYPE(m->hdr) == PAXISIM_MSG_P1B ? HDR_N(m->hdr) : 0u);
+        k += rec_len(m->hdr);
       }
       rem[src] = 0;
     }
@@ -1165,7 +1503,7 @@ static void replica_step(const struct oracle_sim* s, cluster_t* c, uint32_t r, u
     rec_t* m;
     for (src = 0; pick >= rem[src]; src++) pick -= rem[src];
     m = mb_rec(s, c, b, r, src, pos[src]);
-    len = 1u + (HDR_TYPE(m->hdr) == PAXISIM_MSG_P1B ? HDR_N(m->hdr) : 0u);
+    len = rec_len(m->hdr);
     pos[src] += len;
     rem[src] -= len;
     total -= len;
@@ -1173,6 +1511,7 @@ static void replica_step(const struct oracle_sim* s, cluster_t* c, uint32_t r, u
     else x.n->delivered[HDR_TYPE(m->hdr)]++;
     if (s->cfg.protocol == PAXISIM_ABD) abd_dispatch(&x, src, m);
     else if (s->cfg.protocol == PAXISIM_WPAXOS) wpaxos_dispatch(&x, src, m);
+    else if (s->cfg.protocol == PAXISIM_EPAXOS) epaxos_dispatch(&x, src, m);
     else paxos_dispatch(&x, src, m);
   }
   for (src = 0; src < s->NS; src++) *mb_cnt(s, c, b, r, src) = 0;
@@ -1191,7 +1530,10 @@ static void cluster_step(const struct oracle_sim* s, cluster_t* c, uint32_t t) {
 static int check_config(const paxisim_config* cfg, const paxisim_workload* wl,
                         const paxisim_fault_process* fp, uint32_t* N_out) {
   uint32_t z, N = 0, w;
-  if (cfg->protocol > PAXISIM_WPAXOS) return fail(PAXISIM_EUNSUPP, "protocol %u not built", cfg->protocol);
+  if (cfg->protocol > PAXISIM_EPAXOS || cfg->protocol == PAXISIM_M2PAXOS || cfg->protocol == PAXISIM_KPAXOS)
+    return fail(PAXISIM_EUNSUPP, "protocol %u not built", cfg->protocol);
+  if (cfg->protocol == PAXISIM_EPAXOS && (cfg->keys < 1 || cfg->keys > WP_KMAX))
+    return fail(PAXISIM_EINVAL, "EPaxos keys must be in [1,%u]", WP_KMAX);
   if (cfg->protocol == PAXISIM_ABD && (cfg->keys < 1 || cfg->keys > KMAX)) return fail(PAXISIM_EINVAL, "keys");
   if (cfg->protocol == PAXISIM_WPAXOS && (cfg->keys < 1 || cfg->keys > WP_KMAX))
     return fail(PAXISIM_EINVAL, "WPaxos keys must be in [1,%u]", WP_KMAX);
@@ -1207,6 +1549,7 @@ static int check_config(const paxisim_config* cfg, const paxisim_workload* wl,
     N += cfg->npz[z];
   }
   if (N < 1 || N > PAXISIM_MAX_N) return fail(PAXISIM_EINVAL, "N=%u out of range", N);
+  if (cfg->protocol == PAXISIM_EPAXOS && N > 12) return fail(PAXISIM_EINVAL, "EPaxos supports N <= 12");
   if (cfg->window < 8 || cfg->window > PAXISIM_MAX_WINDOW || (cfg->window & (cfg->window - 1)))
     return fail(PAXISIM_EINVAL, "window must be a power of 2 in [8,64]");
   if (cfg->mbox_cap < 2 || cfg->mbox_cap > PAXISIM_MAX_MBOX) return fail(PAXISIM_EINVAL, "mbox_cap");
@@ -1250,6 +1593,16 @@ static void cluster_init(struct oracle_sim* s, cluster_t* c, uint64_t gid, entry
       p->log = logs + ((size_t)r * s->NK + k) * s->W;
       p->exists = s->cfg.protocol != PAXISIM_WPAXOS;
       p->pol_last = POL_NONE;
+    }
+    if (s->cfg.protocol == PAXISIM_EPAXOS) {             /* replica.go:37-47: slot, committed, executed = -1 */
+      replica_t* p = &c->rep[r];
+      uint32_t o;
+      p->ep_log = (ep_inst_t*)calloc((size_t)s->N * s->W, sizeof(ep_inst_t));
+      p->ep_cf = (int32_t*)malloc((size_t)s->N * s->cfg.keys * 2 * sizeof(int32_t));
+      p->ep_maxseq = (int32_t*)malloc((size_t)s->cfg.keys * sizeof(int32_t));
+      for (o = 0; o < s->N * s->cfg.keys; o++) { p->ep_cf[2 * o] = -1; p->ep_cf[2 * o + 1] = 0; }
+      for (o = 0; o < s->cfg.keys; o++) p->ep_maxseq[o] = -1;
+      for (o = 0; o < s->N; o++) p->ep_slot[o] = p->ep_committed[o] = p->ep_executed[o] = -1;
     }
     if (s->cfg.protocol == PAXISIM_ABD) {
       c->rep[r].kv_val = (uint32_t*)calloc(2u * s->cfg.keys, sizeof(uint32_t));
@@ -1307,7 +1660,7 @@ int oracle_create(const paxisim_config* cfg, const paxisim_workload* wl,
   for (z = 0; z < s->wl.outstanding; z++) s->late_workers |= s->wl.start_step[z] != 0;
   s->OW = abd_ow(wl->outstanding);
   s->NK = cfg->protocol == PAXISIM_WPAXOS ? cfg->keys : 1u;
-  s->AR = cfg->protocol == PAXISIM_ABD ? 0u
+  s->AR = (cfg->protocol == PAXISIM_ABD || cfg->protocol == PAXISIM_EPAXOS) ? 0u
           : cfg->agree_ring ? cfg->agree_ring : (cfg->protocol == PAXISIM_WPAXOS ? 128u : 1024u);
   s->q1 = cfg->q1;
   s->q2 = cfg->q2;
@@ -1366,6 +1719,9 @@ int oracle_destroy(oracle_sim* s) {
       free(c->rep[r].kv_val);
       free(c->rep[r].ops);
       free(c->rep[r].hist);
+      free(c->rep[r].ep_log);
+      free(c->rep[r].ep_cf);
+      free(c->rep[r].ep_maxseq);
     }
     free(c->mbox);
     free(c->cnt);
@@ -1504,6 +1860,15 @@ static void fill_state(const struct oracle_sim* s, const cluster_t* c, uint32_t 
     o->execute = ex;
     o->digest = d;
   }
+  if (s->cfg.protocol == PAXISIM_EPAXOS) {         /* own log head, executed prefix over all logs */
+    uint32_t o2;
+    o->ballot = 0;
+    o->slot = p->ep_slot[r];
+    o->execute = 0;
+    for (o2 = 0; o2 < s->N; o2++) o->execute += p->ep_executed[o2] + 1;
+    o->active = o->p1_acks = o->npending = 0;
+    o->executed_writes = p->ep_execs;
+  }
   if (s->cfg.protocol == PAXISIM_ABD) {            /* ABD: op counter, Done ops, KV digest, live ops */
     uint32_t k, live = 0;
     uint64_t d = 0;
@@ -1538,6 +1903,21 @@ int oracle_read_instances(oracle_sim* s, uint64_t lo, uint64_t n, paxisim_instan
   uint32_t r, k;
   if (!s || !out) return fail(PAXISIM_EINVAL, "null argument");
   if (lo + n > s->C) return fail(PAXISIM_ERANGE, "cluster range");
+  if (s->cfg.protocol == PAXISIM_EPAXOS) {         /* one record per (replica, owner log) */
+    for (i = 0; i < n; i++)
+      for (r = 0; r < s->N; r++)
+        for (k = 0; k < s->N; k++) {
+          const replica_t* p = &s->cl[lo + i].rep[r];
+          paxisim_instance_state* o = &out[(i * s->N + r) * s->N + k];
+          memset(o, 0, sizeof *o);
+          o->slot = p->ep_slot[k];
+          o->execute = p->ep_executed[k] + 1;
+          o->p1_acks = (uint32_t)(p->ep_committed[k] + 1);
+          o->exists = 1;
+          o->policy_last = POL_NONE;
+        }
+    return 0;
+  }
   for (i = 0; i < n; i++)
     for (r = 0; r < s->N; r++)
       for (k = 0; k < s->NK; k++) {
@@ -1612,6 +1992,7 @@ int oracle_check(oracle_sim* s, uint64_t* violations) {
     const cluster_t* c = &s->cl[i];
     int bad = 0;
     uint32_t key;
+    if (s->cfg.protocol == PAXISIM_EPAXOS) continue;           /* no single log: paxisim.h */
     for (a = 0; a < s->N; a++) bad |= c->rep[a].agb != 0;      /* running check (agree_arrive) */
     for (key = 0; key < s->NK && !bad; key++)      /* per Paxos instance: WPaxos per key (tla Safety) */
       for (a = 0; a < s->N && !bad; a++)

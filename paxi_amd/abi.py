@@ -6,7 +6,7 @@ structs, so the two speak exactly the same ABI.
 """
 import ctypes as C
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 MAX_N = 16
 MAX_ZONES = 16
 MAX_WORKERS = 32
@@ -22,7 +22,7 @@ ALL_DST = 0xFF
 OK, EINVAL, ENOMEM, EDEVICE, EUNSUPP, ERANGE = 0, -1, -2, -3, -4, -5
 
 # protocols (server/server.go:38-84)
-PAXOS, ABD, WPAXOS, M2PAXOS, KPAXOS = 0, 1, 2, 3, 4
+PAXOS, ABD, WPAXOS, M2PAXOS, KPAXOS, EPAXOS = 0, 1, 2, 3, 4, 5
 PER_KEY = (WPAXOS, M2PAXOS, KPAXOS)   # protocols with one Paxos instance per key
 
 # quorum predicates (quorum.go)
@@ -30,12 +30,14 @@ Q_MAJORITY, Q_ALL, Q_FAST, Q_GRID_ROW, Q_ZONE_MAJORITY, Q_GRID_COLUMN, Q_FGRID_Q
 
 # message types
 (MSG_NONE, MSG_REQUEST, MSG_REPLY, MSG_P1A, MSG_P1B, MSG_P1B_ENTRY, MSG_P2A, MSG_P2B,
- MSG_P3, MSG_GET, MSG_GETREPLY, MSG_SET, MSG_SETREPLY, MSG_LEADERCHG) = range(14)
-NMSG = 16
+ MSG_P3, MSG_GET, MSG_GETREPLY, MSG_SET, MSG_SETREPLY, MSG_LEADERCHG, MSG_PREACCEPT, MSG_PREACCEPTREPLY,
+ MSG_ACCEPT, MSG_ACCEPTREPLY, MSG_COMMIT) = range(19)
+NMSG = 20
 MSG_NAMES = {MSG_REQUEST: "Request", MSG_REPLY: "Reply", MSG_P1A: "P1a", MSG_P1B: "P1b",
              MSG_P2A: "P2a", MSG_P2B: "P2b", MSG_P3: "P3", MSG_GET: "Get",
              MSG_GETREPLY: "GetReply", MSG_SET: "Set", MSG_SETREPLY: "SetReply",
-             MSG_LEADERCHG: "LeaderChange"}
+             MSG_LEADERCHG: "LeaderChange", MSG_PREACCEPT: "PreAccept", MSG_PREACCEPTREPLY: "PreAcceptReply",
+             MSG_ACCEPT: "Accept", MSG_ACCEPTREPLY: "AcceptReply", MSG_COMMIT: "Commit"}
 
 # flags
 F_WOVF, F_GHOST, F_MBOX_OVF, F_PEND_OVF, F_UNFAITHFUL, F_POISON, F_BALLOT_OVF, F_HIST_OVF = (
@@ -264,5 +266,8 @@ def n_replicas(cfg):
 
 
 def n_instances(cfg):
-    """Paxos instances per replica: one kpaxos per key for WPaxos, else one."""
+    """read_instances records per replica: one kpaxos per key (WPaxos, M2Paxos,
+    KPaxos), one per owner log (EPaxos), else one."""
+    if cfg.protocol == EPAXOS:
+        return n_replicas(cfg)
     return cfg.keys if cfg.protocol in PER_KEY else 1

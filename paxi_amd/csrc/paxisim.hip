@@ -16,6 +16,7 @@
 #include <utility>
 #include <vector>
 
+#include "epaxos_kernel.h"
 #include "lin_kernel.h"
 #include "paxisim_dev.h"
 #include "sim_core.h"
@@ -99,6 +100,11 @@ __global__ void init_kernel(Params P) {
         P.wst[2 * si] = make_uint4(0u, 0xFFFFFFFFu, 0u, 0u);
         P.wst[2 * si + 1] = make_uint4(0u, 0u, 0u, POL_NONE);
       }
+  if (P.protocol == PAXISIM_EPAXOS) {                                      // replica.go:37-47: -1 everywhere
+    for (uint32_t k = 0; k < 3 * P.N * P.N; k++) P.ep_sce[(size_t)k * P.C + c] = 0xFFFFFFFFu;
+    for (uint32_t k = 0; k < P.N * P.keys * P.N; k++) P.ep_cf[(size_t)k * P.C + c] = 0xFFFFFFFFu;
+    for (uint32_t k = 0; k < P.keys * P.N; k++) P.ep_max[(size_t)k * P.C + c] = 0xFFFFFFFFu;
+  }
   if (c >= P.clusters) return;
   uint8_t* cnt = img + P.img.off_cnt;
   uint32_t* wcur = reinterpret_cast<uint32_t*>(img + P.img.off_wcur);
@@ -186,6 +192,17 @@ __global__ void gather_kernel(Params P, uint64_t lo, uint64_t n, paxisim_replica
     s.digest = d;
     s.npending = live;
   }
+  if (P.protocol == PAXISIM_EPAXOS) {   // own log head, executed prefix over all logs (paxisim.h)
+    int32_t ex = 0;
+    for (uint32_t o = 0; o < P.N; o++) ex += (int32_t)P.ep_sce[(((size_t)2 * P.N + o) * P.N + r) * P.C + c] + 1;
+    s.ballot = 0;
+    s.slot = (int32_t)P.ep_sce[(((size_t)0 * P.N + r) * P.N + r) * P.C + c];
+    s.execute = ex;
+    s.active = 0;
+    s.p1_acks = 0;
+    s.npending = 0;
+    s.executed_writes = P.execute[j];
+  }
   if (P.protocol == PAXISIM_WPAXOS) {   // aggregate over the key instances (paxisim.h read_state)
     uint32_t hi = 0, led = 0, act = 0, ex = 0, np = 0, em = 0;
     uint64_t d = 0;
@@ -215,6 +232,21 @@ __global__ void gather_kernel(Params P, uint64_t lo, uint64_t n, paxisim_replica
 // read_instances: one record per (cluster, replica, instance)
 __global__ void gather_inst_kernel(Params P, uint64_t lo, uint64_t n, paxisim_instance_state* out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (P.protocol == PAXISIM_EPAXOS) {   // (replica, owner log): slot, executed + 1, committed + 1
+    if (i >= n * P.N * P.N) return;
+    const uint64_t c = slot_of(P, lo + i / (P.N * P.N));
+    const uint32_t r = (uint32_t)((i / P.N) % P.N), o = (uint32_t)(i % P.N);
+    paxisim_instance_state s;
+    memset(&s, 0, sizeof s);
+    auto sce = [&](uint32_t k) { return (int32_t)P.ep_sce[(((size_t)k * P.N + o) * P.N + r) * P.C + c]; };
+    s.slot = sce(0);
+    s.execute = sce(2) + 1;
+    s.p1_acks = (uint32_t)(sce(1) + 1);
+    s.exists = 1;
+    s.policy_last = POL_NONE;
+    out[i] = s;
+    return;
+  }
   if (i >= n * P.NI) return;
   const uint64_t c = slot_of(P, lo + i / P.NI);
   const uint32_t r = (uint32_t)((i / P.NK) % P.N), k = (uint32_t)(i % P.NK);
@@ -268,7 +300,7 @@ __global__ void gather_inst_kernel(Params P, uint64_t lo, uint64_t n, paxisim_in
 __global__ void check_kernel(Params P, uint64_t* out) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t bad = 0;
-  if (c < P.clusters) {
+  if (c < P.clusters && P.protocol != PAXISIM_EPAXOS) {   // EPaxos: no single log (paxisim.h)
     for (uint32_t r = 0; r < P.N; r++) bad |= P.stats[krc(P, ST_AGB, r, c)] != 0;   // running check (paxos_exec)
     auto exec_digest = [&](uint32_t key, uint32_t r, uint32_t& e, uint64_t& d) {
       if (P.protocol == PAXISIM_WPAXOS) {
@@ -561,7 +593,7 @@ static Image proto_image(uint32_t protocol, uint32_t N, uint32_t W, uint32_t K, 
     const uint32_t kv = N * K * LANES * 4u;
     return image_layout(kv, kv, N * abd_ow(WK) * ABD_OPF * LANES * 4u, N, WK, D);
   }
-  if (protocol == PAXISIM_WPAXOS) return image_layout(0, 0, 0, N, WK, D);   // instance state in HBM
+  if (protocol == PAXISIM_WPAXOS || protocol == PAXISIM_EPAXOS) return image_layout(0, 0, 0, N, WK, D);   // state in HBM
   const uint32_t logb = N * W * LANES * 4u;
   return image_layout(logb, logb, logb, N, WK, D);
 }
@@ -569,7 +601,10 @@ static Image proto_image(uint32_t protocol, uint32_t N, uint32_t W, uint32_t K, 
 static int check_config(const paxisim_config* cfg, const paxisim_workload* wl, const paxisim_fault_process* fp,
                         uint32_t* N_out) {
   uint32_t N = 0;
-  if (cfg->protocol > PAXISIM_WPAXOS) return fail(PAXISIM_EUNSUPP, "protocol %u not built", cfg->protocol);
+  if (cfg->protocol > PAXISIM_EPAXOS || cfg->protocol == PAXISIM_M2PAXOS || cfg->protocol == PAXISIM_KPAXOS)
+    return fail(PAXISIM_EUNSUPP, "protocol %u not built", cfg->protocol);
+  if (cfg->protocol == PAXISIM_EPAXOS && (cfg->keys < 1 || cfg->keys > 32))
+    return fail(PAXISIM_EINVAL, "EPaxos keys must be in [1,32]");
   if (cfg->protocol == PAXISIM_ABD && (cfg->keys < 1 || cfg->keys > 64)) return fail(PAXISIM_EINVAL, "keys");
   if (cfg->protocol == PAXISIM_WPAXOS && (cfg->keys < 1 || cfg->keys > 32))
     return fail(PAXISIM_EINVAL, "WPaxos keys must be in [1,32]");
@@ -585,6 +620,7 @@ static int check_config(const paxisim_config* cfg, const paxisim_workload* wl, c
   }
   if (N < 1 || N > PAXISIM_MAX_N) return fail(PAXISIM_EINVAL, "N=%u out of range", N);
   if (cfg->protocol == PAXISIM_ABD && N > 15) return fail(PAXISIM_EINVAL, "ABD supports N <= 15");
+  if (cfg->protocol == PAXISIM_EPAXOS && N > EP_NMAX) return fail(PAXISIM_EINVAL, "EPaxos supports N <= %u", EP_NMAX);
   if (cfg->window < 8 || cfg->window > PAXISIM_MAX_WINDOW || (cfg->window & (cfg->window - 1)))
     return fail(PAXISIM_EINVAL, "window must be a power of 2 in [8,64]");
   if (cfg->mbox_cap < 2 || cfg->mbox_cap > PAXISIM_MAX_MBOX) return fail(PAXISIM_EINVAL, "mbox_cap");
@@ -649,6 +685,7 @@ extern "C" int paxisim_destroy(paxisim* h) {
 static StepOps step_ops_for(uint32_t protocol, uint32_t N) {
   if (protocol == PAXISIM_WPAXOS) return wpaxos_step_ops(N);
   if (protocol == PAXISIM_ABD) return abd_step_ops(N);
+  if (protocol == PAXISIM_EPAXOS) return epaxos_step_ops(N);
   return paxos_step_ops(N);
 }
 
@@ -701,7 +738,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
   P.policy_interval = cfg->policy_interval;
   P.policy_alpha = cfg->policy_alpha;
   P.H = cfg->protocol == PAXISIM_ABD ? cfg->history : 0;
-  P.AR = cfg->protocol == PAXISIM_ABD ? 0u
+  P.AR = (cfg->protocol == PAXISIM_ABD || cfg->protocol == PAXISIM_EPAXOS) ? 0u
          : cfg->agree_ring ? cfg->agree_ring : (cfg->protocol == PAXISIM_WPAXOS ? 128u : 1024u);
   P.OW = abd_ow(wl->outstanding);
   P.W = cfg->window;
@@ -809,6 +846,11 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     uint4* hist = carve<uint4>(p, NC * P.H);
     uint32_t* maps = carve<uint32_t>(p, C * 4);
     unsigned long long* agr = carve<unsigned long long>(p, (size_t)P.AR * P.NK * C);
+    const bool ep = P.protocol == PAXISIM_EPAXOS;
+    uint4* ep_inst = carve<uint4>(p, ep ? (size_t)N * N * P.W * C * 4 : 0);
+    uint32_t* ep_sce = carve<uint32_t>(p, ep ? (size_t)3 * N * N * C : 0);
+    uint32_t* ep_cf = carve<uint32_t>(p, ep ? (size_t)2 * N * P.keys * N * C : 0);
+    uint32_t* ep_max = carve<uint32_t>(p, ep ? (size_t)P.keys * N * C : 0);
     uint8_t* image = carve<uint8_t>(p, blocks * P.img.bytes);
     char* zend = p;
     uint4* rec = carve<uint4>(p, blocks * P.rec_per_block);
@@ -821,6 +863,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
       P.wst = wst; P.wlog = wlog; P.wpend = wpend; P.gst = gst; P.wpx = wpx;
       P.slot_of = maps; P.cl_of = maps + C; P.frz = maps + 2 * C; P.qf = maps + 3 * C;
       P.agr = agr;
+      P.ep_inst = ep_inst; P.ep_sce = ep_sce; P.ep_cf = ep_cf; P.ep_max = ep_max;
     }
     return std::make_pair((size_t)zend, (size_t)p);
   };
@@ -1091,7 +1134,8 @@ extern "C" int paxisim_read_instances(paxisim* h, uint64_t lo, uint64_t n, paxis
   if (lo + n > h->cfg.clusters || lo + n < lo) return fail(PAXISIM_ERANGE, "cluster range");
   if (n == 0) return 0;
   HIPCHK(hipSetDevice(h->cfg.device));
-  const size_t cnt = (size_t)n * h->P.NI;
+  const uint32_t ni = h->P.protocol == PAXISIM_EPAXOS ? h->P.N : h->P.NI;   // EPaxos: one record per owner log
+  const size_t cnt = (size_t)n * ni;
   paxisim_instance_state* d = nullptr;
   HIPCHK(hipMalloc(&d, cnt * sizeof(paxisim_instance_state)));
   gather_inst_kernel<<<(unsigned)((cnt + 255) / 256), 256, 0, h->stream>>>(h->P, lo, n, d);

@@ -143,6 +143,11 @@ struct Params {
   uint32_t variant;      // per-key protocol run by the WPaxos kernel: WPAXOS, M2PAXOS or KPAXOS
   uint32_t zfirst[PAXISIM_MAX_ZONES];   // replica index of "z.1" (KPaxos static leaders)
   uint32_t key_min;      // Bconfig.Min: key value of key index 0
+  // EPaxos (epaxos_kernel.h)
+  uint4* ep_inst;        // [blk][r][o][W][64] x 4 uint4
+  uint32_t* ep_sce;      // [3][o][r][C] slot, committed, executed
+  uint32_t* ep_cf;       // [2][o][K][r][C] conflicts {slot or -1, seq}
+  uint32_t* ep_max;      // [K][r][C] maxSeqPerKey, -1 = absent
 };
 
 // slot of local cluster c
@@ -184,6 +189,12 @@ __device__ __forceinline__ uint32_t mkreq(uint32_t cid, uint32_t o) { return cid
 __device__ __forceinline__ uint32_t hdr_type(uint32_t h) { return h & 0xFFu; }
 __device__ __forceinline__ uint32_t hdr_n(uint32_t h) { return (h >> 8) & 0xFFu; }
 __device__ __forceinline__ uint32_t hdr_key(uint32_t h) { return h >> 16; }
+// records of one message: a P1b and the EPaxos messages carry payload records
+// (ABD keeps its key in bits 8-15, so the count is read only for those types)
+__device__ __forceinline__ uint32_t rec_len(uint32_t h) {
+  const uint32_t t = hdr_type(h);
+  return 1u + ((t == PAXISIM_MSG_P1B || (t >= PAXISIM_MSG_PREACCEPT && t <= PAXISIM_MSG_COMMIT)) ? hdr_n(h) : 0u);
+}
 
 // ---- quorum predicates on an ack mask (quorum.go:55-119) -----------------
 __device__ __forceinline__ bool quorum_ok(const Params& P, uint32_t kind, uint32_t mask) {

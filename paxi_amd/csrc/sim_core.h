@@ -420,7 +420,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
         for (uint32_t k = 0; k < n;) {
           const uint32_t h = ldg(&x.rec[(((box0 + s) * P.M + k) << 6) | x.lane]).x;
           x.discarded++;
-          k += 1u + (hdr_type(h) == PAXISIM_MSG_P1B ? hdr_n(h) : 0u);
+          k += rec_len(h);
         }
         n = 0;
       }
@@ -539,8 +539,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
 #ifdef PXS_STAMPS
     const unsigned long long w0 = stamp();
 #endif
-    const uint32_t type = hdr_type(m.x);
-    const uint32_t len = 1u + (type == PAXISIM_MSG_P1B ? hdr_n(m.x) : 0u);
+    const uint32_t len = rec_len(m.x);
 #pragma unroll
     for (uint32_t s = 0; s < NSMAX; s++) rem[s] = opaque(rem[s]) - (s == src ? len : 0u);
     total -= len;

@@ -24,6 +24,7 @@ struct StepOps {
 StepOps paxos_step_ops(uint32_t N);
 StepOps abd_step_ops(uint32_t N);
 StepOps wpaxos_step_ops(uint32_t N);
+StepOps epaxos_step_ops(uint32_t N);
 
 #ifdef PXS_STEP_INSTANCE   // included by a kernel translation unit
 template <int NT, class Proto>
