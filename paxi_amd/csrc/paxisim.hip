@@ -1134,7 +1134,7 @@ extern "C" int paxisim_read_instances(paxisim* h, uint64_t lo, uint64_t n, paxis
   if (lo + n > h->cfg.clusters || lo + n < lo) return fail(PAXISIM_ERANGE, "cluster range");
   if (n == 0) return 0;
   HIPCHK(hipSetDevice(h->cfg.device));
-  const uint32_t ni = h->P.protocol == PAXISIM_EPAXOS ? h->P.N : h->P.NI;   // EPaxos: one record per owner log
+  const uint32_t ni = h->P.protocol == PAXISIM_EPAXOS ? h->P.N * h->P.N : h->P.NI;   // per cluster; EPaxos: (replica, owner log)
   const size_t cnt = (size_t)n * ni;
   paxisim_instance_state* d = nullptr;
   HIPCHK(hipMalloc(&d, cnt * sizeof(paxisim_instance_state)));
