@@ -679,8 +679,11 @@ template <int NT> constexpr int min_waves() { return NT == 0 ? 4 : 3; }
 // workgroup runs alone on its CU and has LDS to spare (9 replicas, ABD's 3/5);
 // elsewhere the second copy of the loop costs registers the packed cluster
 // groups need.  StepOps::staged exports it (step_ops.h); paxisim.hip sets J = 0 without it.
+#ifndef PXS_STAGE5
+#define PXS_STAGE5 0   // 1: the 5-replica Paxos instance carries the staged loop too (A/B)
+#endif
 template <int NT, class Proto> constexpr bool stage_built() {
-  return Proto::kind == PAXISIM_ABD ? NT != 0 : NT == 9;
+  return Proto::kind == PAXISIM_ABD ? NT != 0 : (NT == 9 || (PXS_STAGE5 && NT == 5 && Proto::kind == PAXISIM_PAXOS));
 }
 
 // The largest workgroup: as many N-wave cluster groups as min_waves slots per

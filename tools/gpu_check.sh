@@ -16,4 +16,4 @@ cat "$OUT/bench.json"
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python "$R/bench.py" --no-cpu-baseline "$@" > "$OUT/prof.log" 2>&1 || { echo "rocprof failed rc=$?"; tail -20 "$OUT/prof.log"; exit 1; }
 find "$OUT/prof" -name '*kernel_stats.csv' -exec cat {} \;
-python3 "$R/tools/prof_timed.py" "$(find "$OUT/prof" -name '*kernel_trace.csv' | head -n1)" 20 "$OUT/bench.json" > "$OUT/prof_timed.json" && cat "$OUT/prof_timed.json"
+python3 "$R/tools/prof_timed.py" "$(find "$OUT/prof" -name '*kernel_trace.csv' | head -n1)" 0 "$OUT/bench.json" > "$OUT/prof_timed.json" && cat "$OUT/prof_timed.json"

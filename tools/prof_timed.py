@@ -3,7 +3,8 @@ kernel trace (the last <steps> dispatches of sim_steps), to set beside
 bench.py's HIP-event average (roofline.avg_launch_ms).  The --stats summary
 averages every dispatch, warm-up included, and warm-up launches are faster
 (earlier simulation state).
-usage: python tools/prof_timed.py <run_kernel_trace.csv> <steps> [bench.json]"""
+usage: python tools/prof_timed.py <run_kernel_trace.csv> <timed launches | 0> [bench.json]
+(0: the timed launch count is read from bench.json's roofline.launches)"""
 import csv
 import json
 import sys
@@ -11,6 +12,8 @@ import sys
 rows = [r for r in csv.DictReader(open(sys.argv[1])) if "sim_steps" in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 steps = int(sys.argv[2])
+if steps == 0:
+    steps = int(json.load(open(sys.argv[3]))["roofline"]["launches"])
 d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
 out = {"kernel": rows[-1]["Kernel_Name"], "dispatches": len(d), "timed": steps,
        "rocprof_avg_timed_ms": sum(d[-steps:]) / steps, "rocprof_avg_all_ms": sum(d) / len(d)}

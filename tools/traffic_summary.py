@@ -32,7 +32,7 @@ def bench_line(log):
 def main():
     cfg, d = int(sys.argv[1]), sys.argv[2]
     b = bench_line(os.path.join(d, "p1.log"))
-    k = b["steps"]
+    k = int(b["roofline"]["launches"])        # timed step-kernel launches
     fetch = per_dispatch(os.path.join(d, "p1", "run_counter_collection.csv"), "FETCH_SIZE")[-k:]
     write = per_dispatch(os.path.join(d, "p2", "run_counter_collection.csv"), "WRITE_SIZE")[-k:]
     fkb, wkb = sum(fetch) / len(fetch), sum(write) / len(write)
@@ -48,6 +48,8 @@ def main():
         "write_size_kb_per_launch": wkb,
         "bytes_per_launch": (2.0 * fkb + wkb) * 1024.0,
         "alg_bytes_per_launch": b["roofline"]["alg_bytes_per_launch"],
+        "build_id": b.get("build_id"),
+        "timed_launches": k,
         "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; "
                   "bytes = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024 (MI355X_MICROARCH.md HBM); "
                   "mean over the timed launches",
