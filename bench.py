@@ -75,7 +75,8 @@ def workload(cfg_id, clusters, base, device, args):
     from paxi_amd import abi
     if cfg_id == 2:
         cfg = abi.make_config(npz=[5], clusters=clusters, cluster_base=base, seed=42, window=args.window,
-                              mbox_cap=args.mbox, max_delay=4, steps_per_launch=LAUNCH_STEPS, device=device)
+                              mbox_cap=args.mbox, max_delay=4, steps_per_launch=LAUNCH_STEPS, device=device,
+                              kv=args.kv)
         wl = abi.make_workload(outstanding=8, target=0)
         fp = abi.make_fault_process(drop_ppm=1000, drop_len=50, slow_ppm=1000, slow_len=50, slow_min=1, slow_max=4)
         return cfg, wl, fp, [], {
@@ -99,7 +100,8 @@ def workload(cfg_id, clusters, base, device, args):
         c = args.crash_step
         cfg = abi.make_config(npz=[3, 3, 3], clusters=clusters, cluster_base=base, seed=42, q1=abi.Q_FGRID_Q1,
                               q2=abi.Q_FGRID_Q2, fz=1, ephemeral_leader=1, window=args.window, mbox_cap=args.mbox,
-                              max_delay=0, steps_per_launch=LAUNCH_STEPS, device=device)
+                              max_delay=0, steps_per_launch=LAUNCH_STEPS, device=device,
+                              kv=args.kv)
         wl = abi.make_workload(outstanding=8, target=[0, 0, 0, 0, 3, 3, 3, 3], start_step=[0, 0, 0, 0, c, c, c, c])
         faults = [abi.make_fault(abi.FAULT_CRASH, 0, step_from=c)]
         return cfg, wl, None, faults, {
@@ -109,7 +111,8 @@ def workload(cfg_id, clusters, base, device, args):
     if cfg_id == 5:
         cfg = abi.make_config(protocol=abi.WPAXOS, npz=[3, 3, 3], keys=8, fz=0, adaptive=1, policy_threshold=3,
                               clusters=clusters, cluster_base=base, seed=42, window=args.window, mbox_cap=args.mbox,
-                              max_delay=0, steps_per_launch=LAUNCH_STEPS, device=device)
+                              max_delay=0, steps_per_launch=LAUNCH_STEPS, device=device,
+                              kv=args.kv)
         wl = abi.make_workload(outstanding=9, target=list(range(9)), locality_ppm=700_000)
         return cfg, wl, None, [], {
             "workload": "BASELINE config 5: WPaxos 3 zones x 3 nodes, 8 keys (kpaxos instances) per cluster, "
@@ -238,6 +241,8 @@ def main():
     ap.add_argument("--history", type=int, default=512, help="config 3: ops recorded per replica")
     ap.add_argument("--crash-step", type=int, default=None,
                     help="config 4: step of the leader crash (default: the first timed step)")
+    ap.add_argument("--kv", type=int, default=1, choices=[0, 1],
+                    help="replicas execute into a Database (db.go Execute) - the reference always does")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     for k, v in DEFAULTS[args.config].items():
@@ -322,7 +327,8 @@ def main():
         desc.update({"tiles_per_cu": occ[0], "lds_per_tile": occ[1], "staged_msgs": occ[2]})
         desc.update({"clusters_per_gpu": args.clusters, "sim_steps_per_step": args.sim_steps,
                      "timed_sim_steps": [args.warmup * args.sim_steps, (args.warmup + args.steps) * args.sim_steps],
-                     "window": args.window, "mbox_cap": cfg.mbox_cap, "parallelism": f"cluster-sharded x{world}"})
+                     "window": args.window, "mbox_cap": cfg.mbox_cap, "parallelism": f"cluster-sharded x{world}",
+                     "database": "kv (db.go Execute per replica)" if cfg.kv or args.config == 3 else "off"})
         bid = build_id()
         out = {
             "metric": METRIC,

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PAXISIM_ABI_VERSION 9
+#define PAXISIM_ABI_VERSION 10
 
 #define PAXISIM_MAX_N        16  /* replicas per cluster (ack masks are u16) */
 #define PAXISIM_MAX_ZONES    16
@@ -163,7 +163,9 @@ typedef struct paxisim_config {
   uint32_t agree_ring;        /* agreement scan: digest checkpoints (every 16 executed slots) kept per
                                  cluster and instance, i.e. the lag in slots / 16 it can bridge;
                                  0 = default (Paxos 1024, WPaxos 128, ABD none) */
-  uint32_t pad0;
+  uint32_t kv;                /* 1: every Paxos / WPaxos / M2Paxos / KPaxos / EPaxos replica keeps the
+                                 Database (db.go:53-134): Execute writes a write's value (its command
+                                 id) to its key and counts database.version; ABD always keeps its KV */
 } paxisim_config;
 
 /* Key distributions of the benchmark's key generator (benchmark.go:202-244,
@@ -231,8 +233,8 @@ typedef struct paxisim_replica_state {
   uint32_t discarded;         /* inbound messages discarded while crashed (socket.go:111-118) */
   uint32_t commits;           /* leader commit events (paxos.go:291-292) / ABD Done */
   uint32_t replies;           /* replies delivered to the client */
-  uint32_t executed_writes;   /* reserved */
-  uint32_t pad;
+  uint32_t executed_writes;   /* kv: database.version, the writes Execute applied (db.go:123-134) */
+  uint32_t executions;        /* Execute calls (EPaxos counts re-executions, epaxos/replica.go:362-383) */
 } paxisim_replica_state;
 
 /* One Paxos instance (read_instances): the single paxos.Paxos of a Multi-Paxos
@@ -364,6 +366,12 @@ int  paxisim_history_load(paxisim* h, uint64_t cluster, uint32_t replica, const 
  * per workgroup), LDS per tile, and messages staged into LDS per
  * replica-step (any pointer but the first may be NULL). */
 int  paxisim_occupancy(paxisim* h, int* blocks_per_cu, uint32_t* lds_bytes, uint32_t* staged);
+
+/* Database.Get (db.go:116-121) for keys [0, n) of one replica of a local
+ * cluster (kv on; ABD: its KV): the value is the command id of the write that
+ * set it, 0 = nil.  A read's reply value (Execute's previous value, db.go:
+ * 103-114) is the value its key held when the command executed. */
+int  paxisim_read_kv(paxisim* h, uint64_t cluster, uint32_t replica, uint32_t* values, uint32_t n);
 
 /* Clusters still stepped: a Paxos cluster whose mailboxes are all empty is at
  * a fixed point (no timers, no retries: paxos/paxos.go) and is frozen and

@@ -205,6 +205,8 @@ typedef struct replica {
   int32_t* ep_cf;                  /* [N][keys][2] {slot or -1, seq} */
   int32_t* ep_maxseq;              /* [keys], -1 = absent */
   uint32_t ep_execs;               /* Execute calls (re-executions included) */
+  uint32_t* db;                    /* kv: Database (db.go) values per key, command id of the last write */
+  uint32_t db_version;             /* database.version */
   /* node.forwards (node.go:35, 165-172) */
   uint32_t nfwd, fwd[FMAX];
   /* socket fault state (socket.go:26-34), random process */
@@ -253,6 +255,7 @@ struct oracle_sim {
   uint32_t variant;                /* per-key protocol (cfg.protocol reads WPAXOS): WPAXOS, M2PAXOS, KPAXOS */
   uint32_t zfirst[PAXISIM_MAX_ZONES]; /* replica index of "z.1" */
   uint32_t AR;                     /* agreement ring: checkpoints kept per (cluster, instance) */
+  int kv;                          /* replicas keep the Database (paxisim_config.kv) */
 };
 
 /* handler context: one replica of one cluster at one step */
@@ -556,6 +559,8 @@ static void replica_handle_request(ctx_t* x, uint32_t req) {
 
 static void paxos_exec(ctx_t* x);
 static void agree_arrive(ctx_t* x, uint32_t k);
+static inline uint32_t wl_key(const struct oracle_sim* s, uint32_t kc, uint32_t cid);
+static inline int wl_write(const struct oracle_sim* s, uint32_t kc, uint32_t cid);
 
 static void paxos_handle_p1a(ctx_t* x, uint32_t mb) {      /* paxos.go:134-162 */
   inst_t* p = x->p;
@@ -760,6 +765,15 @@ static void agree_arrive(ctx_t* x, uint32_t k) {
   if (*a != want) x->n->agb++;
 }
 
+/* Database.Execute (db.go:103-114) when replicas keep the KV: a write's value
+ * (its command id) goes to its key, database.version counts it (put,
+ * db.go:123-134); a read changes nothing. */
+static void kv_exec(ctx_t* x, uint32_t cmd) {
+  if (!x->s->kv || !wl_write(x->s, x->c->kc, cmd)) return;
+  x->n->db[wl_key(x->s, x->c->kc, cmd)] = cmd;
+  x->n->db_version++;
+}
+
 static void paxos_exec(ctx_t* x) {                         /* paxos.go:345-369 */
   inst_t* p = x->p;
   for (;;) {
@@ -771,6 +785,7 @@ static void paxos_exec(ctx_t* x) {                         /* paxos.go:345-369 *
       e->req = 0;
     }
     p->digest = mix64(p->digest ^ (((uint64_t)(uint32_t)p->execute << 32) | e->cmd));
+    kv_exec(x, e->cmd);                                    /* p.Execute(e.command), paxos.go:352 */
     if (x->s->keep_xlog) {
       if (p->nx == p->capx) {
         p->capx = p->capx ? 2 * p->capx : 1024;
@@ -1100,6 +1115,7 @@ static void ep_execute(ctx_t* x) {
       if (i->status != EP_COMMITTED) break;
       p->inst[0].digest = mix64(p->inst[0].digest ^ (((uint64_t)((id << 24) | (uint32_t)sl) << 32) | i->cmd));
       p->ep_execs++;
+      kv_exec(x, i->cmd);
       if (s->keep_xlog) {
         inst_t* q = &p->inst[0];
         if (q->nx == q->capx) {
@@ -1604,6 +1620,7 @@ static void cluster_init(struct oracle_sim* s, cluster_t* c, uint64_t gid, entry
       for (o = 0; o < s->cfg.keys; o++) p->ep_maxseq[o] = -1;
       for (o = 0; o < s->N; o++) p->ep_slot[o] = p->ep_committed[o] = p->ep_executed[o] = -1;
     }
+    if (s->kv) c->rep[r].db = (uint32_t*)calloc(s->cfg.keys ? s->cfg.keys : 1, sizeof(uint32_t));
     if (s->cfg.protocol == PAXISIM_ABD) {
       c->rep[r].kv_val = (uint32_t*)calloc(2u * s->cfg.keys, sizeof(uint32_t));
       c->rep[r].kv_ver = c->rep[r].kv_val + s->cfg.keys;
@@ -1673,6 +1690,7 @@ int oracle_create(const paxisim_config* cfg, const paxisim_workload* wl,
     s->cfg.ephemeral_leader = 0;
   }
   s->variant = variant;
+  s->kv = cfg->kv && cfg->protocol != PAXISIM_ABD;
   if (variant == PAXISIM_M2PAXOS || variant == PAXISIM_KPAXOS) s->q1 = s->q2 = PAXISIM_Q_MAJORITY;
   if (variant == PAXISIM_M2PAXOS) s->cfg.adaptive = 1;      /* m2paxos/replica.go:34-52: no -adaptive switch */
   for (z = 0, r = 0; z < s->Z; r += cfg->npz[z], z++) s->zfirst[z] = r;
@@ -1722,6 +1740,7 @@ int oracle_destroy(oracle_sim* s) {
       free(c->rep[r].ep_log);
       free(c->rep[r].ep_cf);
       free(c->rep[r].ep_maxseq);
+      free(c->rep[r].db);
     }
     free(c->mbox);
     free(c->cnt);
@@ -1867,7 +1886,6 @@ static void fill_state(const struct oracle_sim* s, const cluster_t* c, uint32_t 
     o->execute = 0;
     for (o2 = 0; o2 < s->N; o2++) o->execute += p->ep_executed[o2] + 1;
     o->active = o->p1_acks = o->npending = 0;
-    o->executed_writes = p->ep_execs;
   }
   if (s->cfg.protocol == PAXISIM_ABD) {            /* ABD: op counter, Done ops, KV digest, live ops */
     uint32_t k, live = 0;
@@ -1880,6 +1898,9 @@ static void fill_state(const struct oracle_sim* s, const cluster_t* c, uint32_t 
     o->digest = d;
     o->npending = live;
   }
+  o->executions = s->cfg.protocol == PAXISIM_EPAXOS ? p->ep_execs : s->cfg.protocol == PAXISIM_ABD ? 0u
+                                                                   : (uint32_t)o->execute;
+  o->executed_writes = s->kv ? p->db_version : 0u;
   o->client_requests = p->client_requests;
   o->sent = p->sent;
   o->dropped = p->dropped;
@@ -2214,5 +2235,27 @@ int oracle_history_load(oracle_sim* s, uint64_t cl, uint32_t r, const uint32_t* 
   if (n > s->cfg.history) return fail(PAXISIM_EINVAL, "%u ops exceed history capacity %u", n, s->cfg.history);
   for (j = 0; j < n; j++) memcpy(&s->cl[cl].rep[r].hist[j], ops + 5 * (size_t)j, sizeof(hist_t));
   s->cl[cl].rep[r].nh = n;
+  return 0;
+}
+
+/* Database.Get of keys [0, n) of one replica (kv on; ABD: its KV). */
+int oracle_read_kv(oracle_sim* s, uint64_t cl, uint32_t r, uint32_t* out, uint32_t n) {
+  uint32_t k;
+  if (!s || (n && !out) || cl >= s->C || r >= s->N || n > s->cfg.keys) return fail(PAXISIM_EINVAL, "bad argument");
+  for (k = 0; k < n; k++) {
+    const replica_t* p = &s->cl[cl].rep[r];
+    if (s->cfg.protocol == PAXISIM_ABD) out[k] = p->kv_val[k];
+    else if (s->kv) out[k] = p->db[k];
+    else return fail(PAXISIM_EUNSUPP, "replicas keep no Database (config.kv = 0)");
+  }
+  return 0;
+}
+
+/* The key and kind of command `cid` of a cluster (test support: the checker
+ * recomputes a Database from an execution log). */
+int oracle_command(oracle_sim* s, uint64_t cl, uint32_t cid, uint32_t* key, uint32_t* write) {
+  if (!s || cl >= s->C || !cid) return fail(PAXISIM_EINVAL, "bad argument");
+  if (key) *key = wl_key(s, s->cl[cl].kc, cid);
+  if (write) *write = (uint32_t)wl_write(s, s->cl[cl].kc, cid);
   return 0;
 }

@@ -6,7 +6,7 @@ structs, so the two speak exactly the same ABI.
 """
 import ctypes as C
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 MAX_N = 16
 MAX_ZONES = 16
 MAX_WORKERS = 32
@@ -78,7 +78,7 @@ class Config(C.Structure):
         ("policy", C.c_uint32),
         ("policy_interval", C.c_uint32),
         ("policy_alpha", C.c_double),
-        ("agree_ring", C.c_uint32), ("pad0", C.c_uint32),
+        ("agree_ring", C.c_uint32), ("kv", C.c_uint32),
     ]
 
 
@@ -124,13 +124,14 @@ class ReplicaState(C.Structure):
         ("client_requests", C.c_uint32), ("sent", C.c_uint32),
         ("dropped", C.c_uint32), ("discarded", C.c_uint32),
         ("commits", C.c_uint32), ("replies", C.c_uint32),
-        ("executed_writes", C.c_uint32), ("pad", C.c_uint32),
+        ("executed_writes", C.c_uint32), ("executions", C.c_uint32),
     ]
 
     def as_tuple(self):
         return (self.ballot, self.slot, self.execute, self.active, self.flags, self.digest,
                 self.p1_acks, self.npending, tuple(self.delivered), self.client_requests,
-                self.sent, self.dropped, self.discarded, self.commits, self.replies)
+                self.sent, self.dropped, self.discarded, self.commits, self.replies,
+                self.executed_writes, self.executions)
 
 
 class InstanceState(C.Structure):
@@ -200,6 +201,7 @@ def declare(lib, prefix):
         "inject": (C.c_int, [h, C.c_uint64, C.c_uint32, C.c_uint32]),
         "read_log": (C.c_int, [h, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int32, C.c_uint32, P(LogEntry)]),
         "history_load": (C.c_int, [h, C.c_uint64, C.c_uint32, P(C.c_uint32), C.c_uint32]),
+        "read_kv": (C.c_int, [h, C.c_uint64, C.c_uint32, P(C.c_uint32), C.c_uint32]),
         "last_error": (C.c_char_p, []),
     }
     for name, (res, args) in spec.items():
@@ -213,7 +215,7 @@ def make_config(npz=(5,), protocol=PAXOS, q1=Q_MAJORITY, q2=Q_MAJORITY, fz=0, th
                 ephemeral_leader=0, reply_when_commit=0, adaptive=1, policy_threshold=3,
                 window=16, mbox_cap=16, max_delay=4, keys=16, steps_per_launch=0, device=0,
                 clusters=1, cluster_base=0, seed=1, history=0, policy=POLICY_CONSECUTIVE, policy_interval=1,
-                policy_alpha=0.5, agree_ring=0):
+                policy_alpha=0.5, agree_ring=0, kv=0):
     c = Config()
     c.protocol = protocol
     c.n_zones = len(npz)
@@ -227,6 +229,7 @@ def make_config(npz=(5,), protocol=PAXOS, q1=Q_MAJORITY, q2=Q_MAJORITY, fz=0, th
     c.clusters, c.cluster_base, c.seed = clusters, cluster_base, seed
     c.policy, c.policy_interval, c.policy_alpha = policy, policy_interval, policy_alpha
     c.agree_ring = agree_ring
+    c.kv = kv
     return c
 
 

@@ -188,6 +188,7 @@ __device__ void ep_execute(const Params& P, Rep<NT>& x) {
       if (e.status != EP_COMMITTED) break;
       x.digest = mix64(x.digest ^ (((uint64_t)((id << 24) | (uint32_t)sl) << 32) | e.cmd));
       x.execute++;                                       // Execute calls, re-executions included
+      if (P.kv) kv_exec<NT>(P, x, e.cmd);
       if (e.req) {
         ep_reply<NT>(P, x, e);
         P.ep_inst[ii] = make_uint4(e.cmd, e.req, e.acks | (e.nrep << 16), (uint32_t)e.seq);

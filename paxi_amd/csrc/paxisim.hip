@@ -201,7 +201,6 @@ __global__ void gather_kernel(Params P, uint64_t lo, uint64_t n, paxisim_replica
     s.active = 0;
     s.p1_acks = 0;
     s.npending = 0;
-    s.executed_writes = P.execute[j];
   }
   if (P.protocol == PAXISIM_WPAXOS) {   // aggregate over the key instances (paxisim.h read_state)
     uint32_t hi = 0, led = 0, act = 0, ex = 0, np = 0, em = 0;
@@ -226,6 +225,8 @@ __global__ void gather_kernel(Params P, uint64_t lo, uint64_t n, paxisim_replica
     s.npending = np;
     s.digest = d;
   }
+  s.executions = P.protocol == PAXISIM_EPAXOS ? P.execute[j] : P.protocol == PAXISIM_ABD ? 0u : (uint32_t)s.execute;
+  s.executed_writes = P.kv ? P.kv_ver[j] : 0u;
   out[i] = s;
 }
 
@@ -449,6 +450,8 @@ __device__ void swap_slots(const Params& P, uint64_t p, uint64_t q, uint32_t j) 
   swap_rows(P.gst, (size_t)GMAX * P.NI, C, p, q, j);
   swap_rows(P.stats, (size_t)NSTAT * N, C, p, q, j);
   swap_rows(P.agr, (size_t)P.AR * P.NK, C, p, q, j);
+  swap_rows(P.kv_val, P.kv ? (size_t)P.keys * N : 0, C, p, q, j);
+  swap_rows(P.kv_ver, P.kv ? N : 0, C, p, q, j);
   swap_rows(P.frz, 1, C, p, q, j);
   swap_rows(P.qf, 1, C, p, q, j);
   swap_lanes(P.reqx, (size_t)N * P.W * LANES, (size_t)N * P.W, p, q, j);
@@ -771,7 +774,8 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     P.q2 = PAXISIM_Q_MAJORITY;
   }
   if (P.variant == PAXISIM_M2PAXOS) P.adaptive = 1;
-  P.key_min = wl->key_min;   // m2paxos/replica.go:34-52 has no -adaptive switch
+  P.key_min = wl->key_min;
+  P.kv = cfg->protocol != PAXISIM_ABD && cfg->kv ? 1u : 0u;   // m2paxos/replica.go:34-52 has no -adaptive switch
   P.max_delay = cfg->max_delay;
   P.drop_ppm = fp->drop_ppm;
   P.drop_len = fp->drop_len;
@@ -851,6 +855,8 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     uint32_t* ep_sce = carve<uint32_t>(p, ep ? (size_t)3 * N * N * C : 0);
     uint32_t* ep_cf = carve<uint32_t>(p, ep ? (size_t)2 * N * P.keys * N * C : 0);
     uint32_t* ep_max = carve<uint32_t>(p, ep ? (size_t)P.keys * N * C : 0);
+    uint32_t* kv_val = carve<uint32_t>(p, P.kv ? (size_t)P.keys * N * C : 0);
+    uint32_t* kv_ver = carve<uint32_t>(p, P.kv ? (size_t)N * C : 0);
     uint8_t* image = carve<uint8_t>(p, blocks * P.img.bytes);
     char* zend = p;
     uint4* rec = carve<uint4>(p, blocks * P.rec_per_block);
@@ -864,6 +870,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
       P.slot_of = maps; P.cl_of = maps + C; P.frz = maps + 2 * C; P.qf = maps + 3 * C;
       P.agr = agr;
       P.ep_inst = ep_inst; P.ep_sce = ep_sce; P.ep_cf = ep_cf; P.ep_max = ep_max;
+      P.kv_val = kv_val; P.kv_ver = kv_ver;
     }
     return std::make_pair((size_t)zend, (size_t)p);
   };
@@ -974,6 +981,35 @@ static int wake(paxisim* h, uint64_t cluster) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(h->stream));
   h->bound_host = nb32;
+  return 0;
+}
+
+__global__ void read_kv_kernel(Params P, uint64_t cl, uint32_t r, uint32_t n, uint32_t* out) {
+  const uint32_t k = threadIdx.x + blockIdx.x * blockDim.x;
+  if (k >= n) return;
+  const uint64_t c = slot_of(P, cl);
+  if (P.protocol == PAXISIM_ABD)
+    out[k] = reinterpret_cast<const uint32_t*>(P.image + (c / LANES) * (size_t)P.img.bytes +
+                                               P.img.off_a)[((r * P.keys + k) << 6) | (c % LANES)];
+  else
+    out[k] = P.kv_val[((size_t)k * P.N + r) * P.C + c];
+}
+
+// Database.Get (db.go:116-121) of keys [0, n) of one replica
+extern "C" int paxisim_read_kv(paxisim* h, uint64_t cluster, uint32_t replica, uint32_t* values, uint32_t n) {
+  if (!h || (n && !values)) return fail(PAXISIM_EINVAL, "null argument");
+  if (cluster >= h->cfg.clusters || replica >= h->P.N || n > h->P.keys) return fail(PAXISIM_ERANGE, "bad key range");
+  if (h->P.protocol != PAXISIM_ABD && !h->P.kv) return fail(PAXISIM_EUNSUPP, "replicas keep no Database (config.kv = 0)");
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(h->cfg.device));
+  uint32_t* d = nullptr;
+  HIPCHK(hipMalloc(&d, n * sizeof(uint32_t)));
+  read_kv_kernel<<<(n + 63) / 64, 64, 0, h->stream>>>(h->P, cluster, replica, n, d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(values, d, n * sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(PAXISIM_EDEVICE, "read_kv: %s", hipGetErrorString(e));
   return 0;
 }
 

@@ -148,6 +148,10 @@ struct Params {
   uint32_t* ep_sce;      // [3][o][r][C] slot, committed, executed
   uint32_t* ep_cf;       // [2][o][K][r][C] conflicts {slot or -1, seq}
   uint32_t* ep_max;      // [K][r][C] maxSeqPerKey, -1 = absent
+  // Database (db.go) of the log-based protocols when P.kv
+  uint32_t kv;
+  uint32_t* kv_val;      // [K][r][C] value = command id of the last write, 0 = nil
+  uint32_t* kv_ver;      // [r][C] database.version
 };
 
 // slot of local cluster c

@@ -276,6 +276,17 @@ static __device__ __noinline__ void agree_arrive(unsigned long long* a, uint32_t
   if (st) st0[st * sstride] += 1;
 }
 
+// Database.Execute (db.go:103-114) when replicas keep the KV: a write's value
+// (its command id) goes to its key and database.version counts it (put,
+// db.go:123-134); a read changes nothing.  The previous value Execute returns
+// is what the key holds at this point of the executed log.
+template <int NT>
+__device__ __forceinline__ void kv_exec(const Params& P, Rep<NT>& x, uint32_t cmd) {
+  if (!wl_write(P, x.kc, cmd)) return;
+  P.kv_val[((size_t)wl_key(P, x.kc, cmd) * nrep<NT>(P) + x.r) * P.C + x.c] = cmd;
+  x.kvver++;
+}
+
 template <int NT>
 __device__ __forceinline__ void paxos_exec(const Params& P, Rep<NT>& x) {     // paxos.go:345-369
   for (;;) {
@@ -286,6 +297,7 @@ __device__ __forceinline__ void paxos_exec(const Params& P, Rep<NT>& x) {     //
     const uint32_t cmd = c & CMD_MASK;
     if (c & (EF_REQSELF | EF_REQEXT)) request_reply<NT>(P, x, ereq<NT>(P, x, i, c), cmd);
     x.digest = mix64(x.digest ^ (((uint64_t)(uint32_t)x.execute << 32) | cmd));
+    if (P.kv) kv_exec<NT>(P, x, cmd);                              // p.Execute(e.command), paxos.go:352
     x.l_b[i] = 0u;                                                 // delete(p.log, execute)
     x.execute++;
     if ((uint32_t)x.execute % CKI == 0) {

@@ -36,6 +36,7 @@ struct Rep {
   uint32_t pstride;
   uint32_t dvp[PAXISIM_NMSG / 2];       // delivered by type, two 16-bit counts per word (constant-indexed)
   uint32_t client, sent, dropped, discarded, commits, replies;
+  uint32_t kvver;                       // database.version (P.kv)
   uint32_t send_seq;
   uint32_t dmask, fmask;                // per-step: dropped / flaky destinations
   uint32_t im;                          // pending send intent: destination mask (0 = none)
@@ -735,6 +736,7 @@ __global__ void __launch_bounds__(max_threads<NT>(), min_waves<NT>()) sim_steps(
     const size_t i = rc(P, x.r, x.c);
     x.kc = P.kc[x.c];
     x.flags = P.flags[i];
+    x.kvver = P.kv ? P.kv_ver[i] : 0u;
     Proto::template load<NT>(P, x);
   }
 #pragma unroll
@@ -809,6 +811,7 @@ __global__ void __launch_bounds__(max_threads<NT>(), min_waves<NT>()) sim_steps(
     const uint32_t r = x.r;
     const uint64_t c = x.c;
     P.flags[rc(P, r, c)] = x.flags;
+    if (P.kv) P.kv_ver[rc(P, r, c)] = x.kvver;
     Proto::template store<NT>(P, x);
 #pragma unroll
     for (uint32_t k = 1; k < PAXISIM_NMSG; k++)

@@ -75,7 +75,8 @@ EXPORTED = ["paxisim_abi_version", "paxisim_last_error", "paxisim_create", "paxi
             "paxisim_read_state", "paxisim_read_instances", "paxisim_check", "paxisim_kernel_time", "paxisim_device_bytes",
             "paxisim_linearizable", "paxisim_history", "paxisim_occupancy", "paxisim_inject", "paxisim_read_log",
             "paxisim_history_load", "paxisim_active_clusters", "paxisim_dist_init", "paxisim_dist_unique_id",
-            "paxisim_dist_init_rank", "paxisim_dist_allreduce", "paxisim_dist_stats", "paxisim_dist_destroy"]
+            "paxisim_dist_init_rank", "paxisim_dist_allreduce", "paxisim_dist_stats", "paxisim_dist_destroy",
+            "paxisim_read_kv"]
 
 
 def _check(rc):
@@ -150,6 +151,12 @@ class Simulation:
         buf = (C.c_uint32 * max(1, 5 * n.value))()
         _check(load_library().paxisim_history(self.h, cluster, buf, n.value, C.byref(n)))
         return [tuple(buf[5 * i: 5 * i + 5]) for i in range(n.value)]
+
+    def read_kv(self, cluster, replica, n):
+        """Database.Get (db.go:116-121) of keys [0, n) of one replica (paxisim_read_kv)."""
+        buf = (C.c_uint32 * max(1, n))()
+        _check(load_library().paxisim_read_kv(self.h, cluster, replica, buf, n))
+        return list(buf[:n])
 
     def history_load(self, cluster, replica, ops):
         """History.ReadFile into the device (paxisim_history_load): ops are

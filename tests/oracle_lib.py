@@ -20,6 +20,8 @@ def lib():
             raise RuntimeError(f"oracle not built: run `make -C oracle` ({ORACLE_SO})")
         L = C.CDLL(ORACLE_SO)
         abi.declare(L, "oracle")
+        L.oracle_command.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.POINTER(C.c_uint32),
+                                     C.POINTER(C.c_uint32)]
         L.oracle_step.restype = C.c_int
         L.oracle_step.argtypes = [C.c_void_p, C.c_uint32, C.c_int]
         L.oracle_exec_log.restype = C.c_int
@@ -110,6 +112,17 @@ class OracleSim:
         buf = (C.c_uint32 * max(1, 5 * n.value))()
         _check(lib().oracle_history(self.h, cluster, buf, n.value, C.byref(n)))
         return [tuple(buf[5 * i: 5 * i + 5]) for i in range(n.value)]
+
+    def read_kv(self, cluster, replica, n):
+        buf = (C.c_uint32 * max(1, n))()
+        _check(lib().oracle_read_kv(self.h, cluster, replica, buf, n))
+        return list(buf[:n])
+
+    def command(self, cluster, cid):
+        """(key, is_write) of command `cid` of a cluster, as the workers draw it."""
+        k, w = C.c_uint32(), C.c_uint32()
+        _check(lib().oracle_command(self.h, cluster, cid, C.byref(k), C.byref(w)))
+        return k.value, bool(w.value)
 
     def history_load(self, cluster, replica, ops):
         flat = [int(v) for o in ops for v in o]

@@ -31,7 +31,7 @@ def test_single_write_fast_path(seed):
     assert st["commits"] == 1 and st["replies"] == 1
     assert [o.exec_log(0, r) for r in range(5)] == [[1]] * 5
     s = o.read_state()
-    assert s[0].slot == 0 and all(r.execute == 1 and r.executed_writes == 1 for r in s)
+    assert s[0].slot == 0 and all(r.execute == 1 and r.executions == 1 for r in s)
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
