@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PAXISIM_ABI_VERSION 10
+#define PAXISIM_ABI_VERSION 11
 
 #define PAXISIM_MAX_N        16  /* replicas per cluster (ack masks are u16) */
 #define PAXISIM_MAX_ZONES    16
@@ -286,6 +286,19 @@ typedef struct paxisim_log_entry {
   uint32_t pad;
 } paxisim_log_entry;
 
+/* One socket record of a replica's inbox (paxisim_read_inbox / paxisim_deliver):
+ * the 16-byte record of DESIGN.md §3.2 {hdr = type | n << 8 | key << 16,
+ * ballot (compressed: n << 4 | replica index), slot, cid} and its source
+ * (replica index, or N = the client queue).  A P1b (and an EPaxos message) is
+ * its header record followed by hdr.n payload records from the same source. */
+typedef struct paxisim_inbox_record {
+  uint32_t src;
+  uint32_t hdr;
+  uint32_t ballot;
+  uint32_t slot;
+  uint32_t cid;
+} paxisim_inbox_record;
+
 typedef struct paxisim paxisim;   /* opaque handle */
 
 int  paxisim_abi_version(void);
@@ -311,6 +324,30 @@ int  paxisim_sync(paxisim* h);
  * an external client whose reply reaches no worker.  EINVAL if the replica's
  * client mailbox for that step is full. */
 int  paxisim_inject(paxisim* h, uint64_t cluster, uint32_t replica, uint32_t cid);
+
+/* The records replica `replica` of local cluster `cluster` receives at the
+ * next step, source by source (0..N-1, then the client), each source's in
+ * FIFO order: what transport.go's per-connection gob decoder hands to
+ * node.recv (transport.go:146-165, node.go:79-101) before socket.Recv
+ * (socket.go:111-118).  Sent-and-dropped messages never reach a mailbox
+ * (socket.go:66-109 drops them at the sender).  *n_out is the count (also
+ * when it exceeds cap: then only cap records are written). */
+int  paxisim_read_inbox(paxisim* h, uint64_t cluster, uint32_t replica, paxisim_inbox_record* out,
+                        uint32_t cap, uint32_t* n_out);
+
+/* Key index (0-based: Key = Bconfig.Min + key) and read/write kind of each of
+ * n command ids of local cluster `cluster` (the workload functions of
+ * a command's key and kind are functions of its id). */
+int  paxisim_commands(paxisim* h, uint64_t cluster, const uint32_t* cids, uint32_t n, uint32_t* keys,
+                      uint32_t* writes);
+
+/* Append n records from source `src` (a replica index; N = the client queue)
+ * to replica `replica`'s inbox for the next step, after the ones already
+ * there: a message arriving off a transport, the replay of a trace decoded
+ * from a gob stream (paxi_amd/trace.py).  EINVAL when the bucket is full
+ * (mbox_cap records per link and step). */
+int  paxisim_deliver(paxisim* h, uint64_t cluster, uint32_t replica, uint32_t src,
+                     const paxisim_inbox_record* recs, uint32_t n);
 
 /* Totals over the handle. */
 int  paxisim_stats_get(paxisim* h, paxisim_stats* out);

@@ -1769,6 +1769,46 @@ int oracle_inject(oracle_sim* s, uint64_t cl, uint32_t r, uint32_t cid) {
   return 0;
 }
 
+/* What replica r of cluster cl receives at the next step, source by source,
+ * FIFO within a source: what a per-connection gob decoder hands node.recv
+ * (transport.go:146-165, node.go:79-101); paxisim_read_inbox. */
+int oracle_read_inbox(oracle_sim* s, uint64_t cl, uint32_t r, paxisim_inbox_record* out, uint32_t cap,
+                      uint32_t* n_out) {
+  cluster_t* c;
+  uint32_t src, k, n = 0;
+  if (!s || !n_out || (cap && !out) || cl >= s->C || r >= s->N) return fail(PAXISIM_EINVAL, "bad inbox");
+  c = &s->cl[cl];
+  for (src = 0; src < s->NS; src++) {
+    const uint32_t kn = *mb_cnt(s, c, s->t % s->D, r, src);
+    for (k = 0; k < kn; k++, n++) {
+      const rec_t* m = mb_rec(s, c, s->t % s->D, r, src, k);
+      if (n >= cap) continue;
+      out[n].src = src; out[n].hdr = m->hdr; out[n].ballot = m->ballot; out[n].slot = m->slot; out[n].cid = m->cid;
+    }
+  }
+  *n_out = n;
+  return 0;
+}
+
+/* A message off a transport (paxisim_deliver): appended to (r, src) for the next step. */
+int oracle_deliver(oracle_sim* s, uint64_t cl, uint32_t r, uint32_t src, const paxisim_inbox_record* in,
+                   uint32_t n) {
+  cluster_t* c;
+  uint8_t* cnt;
+  uint32_t i;
+  if (!s || (n && !in) || cl >= s->C || r >= s->N || src > s->N) return fail(PAXISIM_EINVAL, "bad deliver");
+  if (n == 0) return 0;
+  c = &s->cl[cl];
+  cnt = mb_cnt(s, c, s->t % s->D, r, src);
+  if (*cnt + n > s->M) return fail(PAXISIM_EINVAL, "mailbox full");
+  for (i = 0; i < n; i++) {
+    rec_t* m = mb_rec(s, c, s->t % s->D, r, src, *cnt + i);
+    m->hdr = in[i].hdr; m->ballot = in[i].ballot; m->slot = in[i].slot; m->cid = in[i].cid;
+  }
+  *cnt = (uint8_t)(*cnt + n);
+  return 0;
+}
+
 int oracle_read_log(oracle_sim* s, uint64_t cl, uint32_t r, uint32_t key, int32_t lo, uint32_t n,
                     paxisim_log_entry* out) {
   const inst_t* p;

@@ -34,6 +34,10 @@ int  oracle_read_instances(oracle_sim* h, uint64_t cluster_lo, uint64_t n,
                            paxisim_instance_state* out);
 int  oracle_check(oracle_sim* h, uint64_t* violations);
 int  oracle_inject(oracle_sim* h, uint64_t cluster, uint32_t replica, uint32_t cid);
+int  oracle_read_inbox(oracle_sim* h, uint64_t cluster, uint32_t replica, paxisim_inbox_record* out,
+                       uint32_t cap, uint32_t* n_out);
+int  oracle_deliver(oracle_sim* h, uint64_t cluster, uint32_t replica, uint32_t src,
+                    const paxisim_inbox_record* recs, uint32_t n);
 int  oracle_read_log(oracle_sim* h, uint64_t cluster, uint32_t replica, uint32_t key, int32_t slot_lo,
                      uint32_t n, paxisim_log_entry* out);
 /* Executed command ids of (cluster, replica | key << 16), in slot order (KAT support). */

@@ -6,7 +6,7 @@ structs, so the two speak exactly the same ABI.
 """
 import ctypes as C
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 MAX_N = 16
 MAX_ZONES = 16
 MAX_WORKERS = 32
@@ -165,6 +165,15 @@ class LogEntry(C.Structure):
         return (self.ballot, self.slot, self.cmd, self.flags, self.acks, self.request)
 
 
+class InboxRecord(C.Structure):
+    """One record of a replica's next-step inbox (paxisim_read_inbox / paxisim_deliver)."""
+    _fields_ = [("src", C.c_uint32), ("hdr", C.c_uint32), ("ballot", C.c_uint32), ("slot", C.c_uint32),
+                ("cid", C.c_uint32)]
+
+    def as_tuple(self):
+        return (self.src, self.hdr, self.ballot, self.slot, self.cid)
+
+
 class Stats(C.Structure):
     _fields_ = [
         ("steps", C.c_uint64), ("clusters", C.c_uint64),
@@ -202,6 +211,8 @@ def declare(lib, prefix):
         "read_log": (C.c_int, [h, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int32, C.c_uint32, P(LogEntry)]),
         "history_load": (C.c_int, [h, C.c_uint64, C.c_uint32, P(C.c_uint32), C.c_uint32]),
         "read_kv": (C.c_int, [h, C.c_uint64, C.c_uint32, P(C.c_uint32), C.c_uint32]),
+        "read_inbox": (C.c_int, [h, C.c_uint64, C.c_uint32, P(InboxRecord), C.c_uint32, P(C.c_uint32)]),
+        "deliver": (C.c_int, [h, C.c_uint64, C.c_uint32, C.c_uint32, P(InboxRecord), C.c_uint32]),
         "last_error": (C.c_char_p, []),
     }
     for name, (res, args) in spec.items():

@@ -353,6 +353,57 @@ __global__ void inject_kernel(Params P, uint64_t cl, uint32_t r, uint32_t b, uin
   *status = 0;
 }
 
+// paxisim_read_inbox: replica r's bucket b, source by source, FIFO order
+__global__ void read_inbox_kernel(Params P, uint64_t cl, uint32_t r, uint32_t b, paxisim_inbox_record* out,
+                                  uint32_t cap, uint32_t* n_out) {
+  if (threadIdx.x != 0) return;
+  const uint64_t c = slot_of(P, cl);
+  const uint32_t blk = (uint32_t)(c / LANES), lane = (uint32_t)(c % LANES);
+  const uint8_t* cnt = P.image + (size_t)blk * P.img.bytes + P.img.off_cnt;
+  const uint4* rec = P.rec + (size_t)blk * P.rec_per_block;
+  uint32_t n = 0;
+  for (uint32_t src = 0; src < P.NS; src++) {
+    const uint32_t box = (b * P.N + r) * P.NS + src;
+    const uint32_t k_n = cnt[(box << 6) | lane];
+    for (uint32_t k = 0; k < k_n; k++, n++) {
+      if (n >= cap) continue;
+      const uint4 m = rec[((box * P.M + k) << 6) | lane];
+      out[n] = paxisim_inbox_record{src, m.x, m.y, m.z, m.w};
+    }
+  }
+  *n_out = n;
+}
+
+// paxisim_deliver: n records appended to (bucket b, dst r, src)
+__global__ void deliver_kernel(Params P, uint64_t cl, uint32_t r, uint32_t src, uint32_t b,
+                               const paxisim_inbox_record* in, uint32_t n, uint32_t* status) {
+  if (threadIdx.x != 0) return;
+  const uint64_t c = slot_of(P, cl);
+  const uint32_t blk = (uint32_t)(c / LANES), lane = (uint32_t)(c % LANES);
+  uint8_t* cnt = P.image + (size_t)blk * P.img.bytes + P.img.off_cnt;
+  const uint32_t box = (b * P.N + r) * P.NS + src;
+  const uint32_t k = cnt[(box << 6) | lane];
+  if (k + n > P.M) {
+    *status = 1;
+    return;
+  }
+  uint4* rec = P.rec + (size_t)blk * P.rec_per_block;
+  for (uint32_t i = 0; i < n; i++)
+    rec[(((box * P.M + k + i) << 6) | lane)] = make_uint4(in[i].hdr, in[i].ballot, in[i].slot, in[i].cid);
+  cnt[(box << 6) | lane] = (uint8_t)(k + n);
+  *status = 0;
+}
+
+// paxisim_commands: the workload's key and kind of each command id
+__global__ void command_kernel(Params P, uint64_t cl, const uint32_t* cids, uint32_t n, uint32_t* keys,
+                               uint32_t* writes) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t kc = P.kc[slot_of(P, cl)];
+  keys[i] = wl_key(P, kc, cids[i]);
+  writes[i] = wl_write(P, kc, cids[i]) ? 1u : 0u;
+}
+
 // paxisim_read_log: one thread per slot of one instance's window
 __global__ void read_log_kernel(Params P, uint64_t cl, uint32_t r, uint32_t key, int32_t lo, uint32_t n,
                                 paxisim_log_entry* out) {
@@ -1100,6 +1151,80 @@ extern "C" int paxisim_inject(paxisim* h, uint64_t cluster, uint32_t replica, ui
   return 0;
 }
 
+extern "C" int paxisim_read_inbox(paxisim* h, uint64_t cluster, uint32_t replica, paxisim_inbox_record* out,
+                                  uint32_t cap, uint32_t* n_out) {
+  if (!h || !n_out || (cap && !out)) return fail(PAXISIM_EINVAL, "null argument");
+  if (cluster >= h->cfg.clusters || replica >= h->P.N) return fail(PAXISIM_ERANGE, "bad inbox");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  const uint32_t maxn = h->P.NS * h->P.M;   // a bucket set holds at most this many
+  paxisim_inbox_record* d = nullptr;
+  HIPCHK(hipMalloc(&d, maxn * sizeof(paxisim_inbox_record) + 64));
+  uint32_t* dn = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(d) + maxn * sizeof(paxisim_inbox_record));
+  read_inbox_kernel<<<1, 64, 0, h->stream>>>(h->P, cluster, replica, h->t % h->P.D, d, maxn, dn);
+  hipError_t e = hipGetLastError();
+  uint32_t n = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(&n, dn, sizeof n, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (e == hipSuccess && cap)
+    e = hipMemcpy(out, d, (n < cap ? n : cap) * sizeof(paxisim_inbox_record), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(PAXISIM_EDEVICE, "read_inbox: %s", hipGetErrorString(e));
+  *n_out = n;
+  return 0;
+}
+
+extern "C" int paxisim_commands(paxisim* h, uint64_t cluster, const uint32_t* cids, uint32_t n, uint32_t* keys,
+                                uint32_t* writes) {
+  if (!h || (n && (!cids || !keys || !writes))) return fail(PAXISIM_EINVAL, "null argument");
+  if (cluster >= h->cfg.clusters) return fail(PAXISIM_ERANGE, "bad cluster");
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(h->cfg.device));
+  uint32_t* d = nullptr;
+  HIPCHK(hipMalloc(&d, 3ull * n * sizeof(uint32_t)));
+  hipError_t e = hipMemcpyAsync(d, cids, n * sizeof(uint32_t), hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) {
+    command_kernel<<<(n + 255) / 256, 256, 0, h->stream>>>(h->P, cluster, d, n, d + n, d + 2 * n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(keys, d + n, n * sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(writes, d + 2 * n, n * sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(PAXISIM_EDEVICE, "commands: %s", hipGetErrorString(e));
+  return 0;
+}
+
+extern "C" int paxisim_deliver(paxisim* h, uint64_t cluster, uint32_t replica, uint32_t src,
+                               const paxisim_inbox_record* recs, uint32_t n) {
+  if (!h || (n && !recs)) return fail(PAXISIM_EINVAL, "null argument");
+  if (cluster >= h->cfg.clusters || replica >= h->P.N || src > h->P.N)
+    return fail(PAXISIM_EINVAL, "bad deliver (cluster %llu, replica %u, src %u)", (unsigned long long)cluster,
+                replica, src);
+  if (n == 0) return 0;
+  if (n > h->P.M) return fail(PAXISIM_EINVAL, "mailbox full");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  if (h->P.compact) {
+    const int rc = wake(h, cluster);
+    if (rc) return rc;
+  }
+  paxisim_inbox_record* d = nullptr;
+  HIPCHK(hipMalloc(&d, n * sizeof(paxisim_inbox_record)));
+  hipError_t e = hipMemcpyAsync(d, recs, n * sizeof(paxisim_inbox_record), hipMemcpyHostToDevice, h->stream);
+  uint32_t st = 0;
+  if (e == hipSuccess) {
+    deliver_kernel<<<1, 64, 0, h->stream>>>(h->P, cluster, replica, src, h->t % h->P.D, d, n,
+                                            (uint32_t*)h->d_scratch);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(&st, h->d_scratch, sizeof st, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(PAXISIM_EDEVICE, "deliver: %s", hipGetErrorString(e));
+  if (st) return fail(PAXISIM_EINVAL, "mailbox full");
+  return 0;
+}
+
 extern "C" int paxisim_read_log(paxisim* h, uint64_t cluster, uint32_t replica, uint32_t key, int32_t slot_lo,
                                 uint32_t n, paxisim_log_entry* out) {
   if (!h || !out) return fail(PAXISIM_EINVAL, "null argument");
@@ -1516,7 +1641,7 @@ extern "C" int paxisim_dist_stats(paxisim_dist* d, paxisim_stats* out, double* k
 // Diagnostic build only: per (block, replica) {setup, loop, barrier cycles, loop trips, records, steps}.
 extern "C" int paxisim_dbg_enable(paxisim* h) {
   HIPCHK(hipSetDevice(h->cfg.device));
-  const size_t n = (h->P.C / LANES) * 16 * 16;
+  const size_t n = (h->P.C / LANES) * 16 * DBG_PER;
   HIPCHK(hipMalloc(&h->P.dbg, n * 8));
   HIPCHK(hipMemset(h->P.dbg, 0, n * 8));
   return 0;
@@ -1524,7 +1649,7 @@ extern "C" int paxisim_dbg_enable(paxisim* h) {
 extern "C" int paxisim_dbg_read(paxisim* h, unsigned long long* out) {
   HIPCHK(hipSetDevice(h->cfg.device));
   HIPCHK(hipStreamSynchronize(h->stream));
-  const size_t n = (h->P.C / LANES) * 16 * 16;
+  const size_t n = (h->P.C / LANES) * 16 * DBG_PER;
   HIPCHK(hipMemcpy(out, h->P.dbg, n * 8, hipMemcpyDeviceToHost));
   HIPCHK(hipMemset(h->P.dbg, 0, n * 8));
   return 0;

@@ -113,7 +113,7 @@ struct Params {
   uint32_t *link_drop, *link_slow;  // [dst][N][C]: drop_until; slow_until | delay << 28
   uint32_t* ck_e;        // [CKR][NI][C]
   uint64_t* ck_d;        // [CKR][NI][C]
-  uint4* gst;            // [GMAX][NI][C] entries below execute {slot, ballot, until | commit << 31, 0}
+  uint4* gst;            // entries below execute {slot, ballot, until | commit << 31, 0}: [GMAX][NI][C], per-key instances [NI][C][GMAX]
   // WPaxos kpaxos instances, one 32-B state + a W-entry window + PMAX pending per
   // (blk, key, r, lane): {ballot, slot, execute, active|exists<<1|p1acks<<16,
   // npend, digest lo, digest hi, policy last|hits<<8}; entries {ballot, cmd|flags, acks, request}
@@ -271,6 +271,32 @@ __device__ __forceinline__ bool scripted(const Params& P, uint32_t kind, uint64_
   }
   return hit;
 }
+
+// ---- diagnostic build (PXS_STAMPS): s_memtime phase and per-handler stamps ----
+#ifdef PXS_STAMPS
+constexpr uint32_t DBG_PER = 48;   // per (block, replica): 16 phase totals, 16 handler cycles, 16 handler runs
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+// cycles a wave spent in handler path k this trip (its lanes' branch runs once)
+__device__ __forceinline__ void stamp_case(const Params& P, uint32_t blk, uint32_t r, uint32_t k, uint32_t c0) {
+  const unsigned long long d = (uint32_t)stamp() - c0;   // 32-bit: a 64-bit stamp spilled trips a gfx950 codegen bug
+  if (!P.dbg) return;
+  const unsigned long long act = __ballot(1);
+  if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)act) - 1)) {
+    unsigned long long* q = &P.dbg[((size_t)blk * 16 + r) * DBG_PER];
+    atomicAdd(&q[16 + k], d);
+    atomicAdd(&q[32 + k], 1ull);
+  }
+}
+#define PXS_CASE_T0 const uint32_t pxs_c0 = (uint32_t)stamp();
+#define PXS_CASE_T1(k) if constexpr (NT != 0) stamp_case(P, x.blk, x.r, (k), pxs_c0);   // (NT = 0: a spill codegen bug)
+#else
+#define PXS_CASE_T0
+#define PXS_CASE_T1(k)
+#endif
 
 // ---- SoA addressing --------------------------------------------------------
 __device__ __forceinline__ size_t rc(const Params& P, uint32_t r, uint64_t c) { return (size_t)r * P.C + c; }

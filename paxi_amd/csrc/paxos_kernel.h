@@ -18,43 +18,103 @@ namespace pxs {
 // ---------------------------------------------------------------------------
 struct Ent { uint32_t b, c, a; };
 
+// Two layouts share these handlers.  Multi-Paxos keeps each replica's window
+// in LDS as three u32 planes (l_a / l_b / l_c, entry stride es = 64 lanes) and
+// the request side table in HBM (reqx).  The per-key instances of WPaxos keep
+// theirs in HBM as one 16-B entry {ballot, cmd|flags, acks, request} per slot
+// (es = 4 words): reads go through a one-entry register cache that the
+// dispatcher fills before the handler runs (its load overlaps the instance
+// bind), and writes go through to HBM.  es is a compile-time constant of each
+// kernel instance (sim_steps sets it before any use), so the branch folds.
 template <int NT>
 __device__ __forceinline__ uint32_t eidx(const Params& P, const Rep<NT>& x, int32_t s) {
   return x.e0 + ((uint32_t)s & (P.W - 1u)) * x.es;
 }
 template <int NT>
-__device__ __forceinline__ Ent eget(const Rep<NT>& x, uint32_t i) { return Ent{x.l_a[i], x.l_b[i], x.l_c[i]}; }
+__device__ __forceinline__ bool hbm_log(const Rep<NT>& x) { return x.es == 4u; }
+template <int NT>
+__device__ __forceinline__ void ecache(Rep<NT>& x, uint32_t i) {
+  if (x.ci != i) {
+    x.ce = *reinterpret_cast<const uint4*>(x.l_a + i);
+    x.ci = i;
+  }
+}
+template <int NT>
+__device__ __forceinline__ uint32_t ea(Rep<NT>& x, uint32_t i) {
+  if (hbm_log(x)) { ecache(x, i); return x.ce.x; }
+  return x.l_a[i];
+}
+template <int NT>
+__device__ __forceinline__ uint32_t eb(Rep<NT>& x, uint32_t i) {
+  if (hbm_log(x)) { ecache(x, i); return x.ce.y; }
+  return x.l_b[i];
+}
+template <int NT>
+__device__ __forceinline__ uint32_t ec(Rep<NT>& x, uint32_t i) {
+  if (hbm_log(x)) { ecache(x, i); return x.ce.z; }
+  return x.l_c[i];
+}
+template <int NT>
+__device__ __forceinline__ void set_a(Rep<NT>& x, uint32_t i, uint32_t v) {
+  if (hbm_log(x)) { x.l_a[i] = v; if (x.ci == i) x.ce.x = v; return; }
+  x.l_a[i] = v;
+}
+template <int NT>
+__device__ __forceinline__ void set_b(Rep<NT>& x, uint32_t i, uint32_t v) {
+  if (hbm_log(x)) { x.l_a[i + 1u] = v; if (x.ci == i) x.ce.y = v; return; }
+  x.l_b[i] = v;
+}
+template <int NT>
+__device__ __forceinline__ void set_c(Rep<NT>& x, uint32_t i, uint32_t v) {
+  if (hbm_log(x)) { x.l_a[i + 2u] = v; if (x.ci == i) x.ce.z = v; return; }
+  x.l_c[i] = v;
+}
+template <int NT>
+__device__ __forceinline__ Ent eget(Rep<NT>& x, uint32_t i) { return Ent{ea(x, i), eb(x, i), ec(x, i)}; }
 template <int NT>
 __device__ __forceinline__ void eput(Rep<NT>& x, uint32_t i, const Ent& e) {
+  if (hbm_log(x)) {                                  // one 12-B store
+    uint32_t* q = x.l_a + i;
+    *reinterpret_cast<uint2*>(q) = make_uint2(e.b, e.c);
+    q[2] = e.a;
+    if (x.ci == i) { x.ce.x = e.b; x.ce.y = e.c; x.ce.z = e.a; }
+    return;
+  }
   x.l_a[i] = e.b;
   x.l_b[i] = e.c;
   x.l_c[i] = e.a;
 }
-// request side table slot for LDS entry index i
+// request side table entry for log entry index i
 template <int NT>
-__device__ __forceinline__ uint32_t* reqx_at(const Params& P, const Rep<NT>& x, uint32_t i) {
-  return &x.reqx[i];
+__device__ __forceinline__ uint32_t rq_get(Rep<NT>& x, uint32_t i) {
+  if (hbm_log(x)) { ecache(x, i); return x.ce.w; }
+  return ldg(&x.reqx[i]);
 }
 template <int NT>
-__device__ __forceinline__ uint32_t ereq(const Params& P, const Rep<NT>& x, uint32_t i, uint32_t c) {
+__device__ __forceinline__ void rq_set(Rep<NT>& x, uint32_t i, uint32_t q) {
+  if (hbm_log(x)) { x.l_a[i + 3u] = q; if (x.ci == i) x.ce.w = q; return; }
+  x.reqx[i] = q;
+}
+template <int NT>
+__device__ __forceinline__ uint32_t ereq(const Params& P, Rep<NT>& x, uint32_t i, uint32_t c) {
   if (c & EF_REQSELF) return mkreq(c & CMD_MASK, PAXISIM_CLIENT_SRC);
-  if (c & EF_REQEXT) return ldg(reqx_at(P, x, i));
+  if (c & EF_REQEXT) return rq_get(x, i);
   return 0u;
 }
 // attach request q to entry flags c (whose command is cmd)
 template <int NT>
-__device__ __forceinline__ uint32_t eset_req(const Params& P, const Rep<NT>& x, uint32_t i, uint32_t c, uint32_t q) {
+__device__ __forceinline__ uint32_t eset_req(const Params& P, Rep<NT>& x, uint32_t i, uint32_t c, uint32_t q) {
   c &= ~(EF_REQSELF | EF_REQEXT);
   if (!q) return c;
   if (req_origin(q) == PAXISIM_CLIENT_SRC && req_cid(q) == (c & CMD_MASK)) return c | EF_REQSELF;
-  *reqx_at(P, x, i) = q;
+  rq_set(x, i, q);
   return c | EF_REQEXT;
 }
 // replace the command of an entry, keeping its request (paxos.go:168-171)
 template <int NT>
-__device__ __forceinline__ uint32_t eset_cmd(const Params& P, const Rep<NT>& x, uint32_t i, uint32_t c, uint32_t cmd) {
+__device__ __forceinline__ uint32_t eset_cmd(const Params& P, Rep<NT>& x, uint32_t i, uint32_t c, uint32_t cmd) {
   if ((c & EF_REQSELF) && (c & CMD_MASK) != cmd) {
-    *reqx_at(P, x, i) = mkreq(c & CMD_MASK, PAXISIM_CLIENT_SRC);
+    rq_set(x, i, mkreq(c & CMD_MASK, PAXISIM_CLIENT_SRC));
     c = (c & ~EF_REQSELF) | EF_REQEXT;
   }
   return (c & ~CMD_MASK) | cmd;
@@ -71,12 +131,30 @@ __device__ __forceinline__ void request_reply(const Params& P, Rep<NT>& x, uint3
 }
 
 // node.Forward (node.go:165-172)
+// index of cid in the forwards table, or nfwd: four probes per round trip
+template <int NT>
+__device__ __forceinline__ uint32_t fwd_find(const Params& P, const Rep<NT>& x, uint32_t cid) {
+  if (!hbm_log(x)) {                                     // (A/B r2: the LDS-window kernels keep one probe per trip)
+    uint32_t i = 0;
+    for (; i < x.nfwd; i++)
+      if (req_cid(ldg(&P.fwd[krc(P, i, x.r, x.c)])) == cid) break;
+    return i;
+  }
+  for (uint32_t i = 0; i < x.nfwd; i += 4u) {
+    uint32_t f[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; k++) f[k] = i + k < x.nfwd ? P.fwd[krc(P, i + k, x.r, x.c)] : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; k++)
+      if (i + k < x.nfwd && req_cid(f[k]) == cid) return i + k;
+  }
+  return x.nfwd;
+}
+
 template <int NT>
 __device__ __forceinline__ void node_forward(const Params& P, Rep<NT>& x, uint32_t to, uint32_t req) {
   const uint32_t cid = req_cid(req);
-  uint32_t i = 0;
-  for (; i < x.nfwd; i++)
-    if (req_cid(ldg(&P.fwd[krc(P, i, x.r, x.c)])) == cid) break;
+  const uint32_t i = fwd_find<NT>(P, x, cid);
   if (i == x.nfwd) {
     if (x.nfwd == FMAX) x.flags |= PAXISIM_F_PEND_OVF | PAXISIM_F_UNFAITHFUL;
     else P.fwd[krc(P, x.nfwd++, x.r, x.c)] = req;
@@ -89,9 +167,7 @@ __device__ __forceinline__ void node_forward(const Params& P, Rep<NT>& x, uint32
 // node.recv Reply case (node.go:83-90)
 template <int NT>
 __device__ __forceinline__ void handle_reply(const Params& P, Rep<NT>& x, uint32_t cid) {
-  uint32_t i = 0;
-  for (; i < x.nfwd; i++)
-    if (req_cid(ldg(&P.fwd[krc(P, i, x.r, x.c)])) == cid) break;
+  const uint32_t i = fwd_find<NT>(P, x, cid);
   if (i == x.nfwd) {
     x.flags |= PAXISIM_F_UNFAITHFUL;
     return;
@@ -122,16 +198,22 @@ __device__ __forceinline__ void raise_win(Rep<NT>& x, uint32_t f) {
 // steps of the execution: a ghost lives that long after it is (re)created,
 // in a per-instance table in HBM {slot, ballot, until | commit << 31} touched
 // only on these paths.  iflags GHOST = the table may hold a live entry.
+// Ghost table addressing.  Per-key instances (HBM log) keep a lane's GMAX
+// ghosts of one instance in one 128-B line ([NI][C][GMAX]), so the probes
+// after the first hit in cache; Multi-Paxos keeps [GMAX][NI][C] (A/B r2: the
+// line layout costs its LDS-window kernels registers).  The probes stay
+// serial (ldg): eight in flight at once would cost 32 registers.
 template <int NT>
-__device__ __forceinline__ size_t gidx(const Params& P, const Rep<NT>& x, uint32_t g) {
-  return ((size_t)g * P.NI + x.inst) * P.C + x.c;
+__device__ __forceinline__ uint4* gref(const Params& P, const Rep<NT>& x, uint32_t g) {
+  if (hbm_log(x)) return &P.gst[((size_t)x.inst * P.C + x.c) * GMAX + g];
+  return &P.gst[((size_t)g * P.NI + x.inst) * P.C + x.c];
 }
 template <int NT>
 __device__ __forceinline__ uint32_t ghost_find(const Params& P, Rep<NT>& x, int32_t s, uint4& e) {
   if (!(x.iflags & PAXISIM_F_GHOST)) return GMAX;
   uint32_t live = 0, hit = GMAX;
   for (uint32_t g = 0; g < GMAX; g++) {
-    const uint4 v = ldg(&P.gst[gidx<NT>(P, x, g)]);
+    const uint4 v = ldg(gref<NT>(P, x, g));
     const bool l = (v.z & 0x7FFFFFFFu) > x.t;
     live |= l;
     if (l && v.x == (uint32_t)s && hit == GMAX) { e = v; hit = g; }
@@ -143,7 +225,7 @@ template <int NT>
 __device__ __forceinline__ uint32_t ghost_alloc(const Params& P, Rep<NT>& x) {
   x.flags |= PAXISIM_F_GHOST;
   for (uint32_t g = 0; g < GMAX; g++) {
-    const uint32_t until = ldg(&P.gst[gidx<NT>(P, x, g)]).z & 0x7FFFFFFFu;
+    const uint32_t until = ldg(gref<NT>(P, x, g)).z & 0x7FFFFFFFu;
     if (!(x.iflags & PAXISIM_F_GHOST) || until <= x.t) {
       x.iflags |= PAXISIM_F_GHOST;
       return g;
@@ -162,10 +244,10 @@ __device__ __forceinline__ void ghost(const Params& P, Rep<NT>& x, int32_t s, ui
   uint4 e;
   uint32_t g = ghost_find<NT>(P, x, s, e);
   if (g < GMAX) {
-    if (!(e.z >> 31) && b > e.y) P.gst[gidx<NT>(P, x, g)] = make_uint4(e.x, b, e.z, 0u);
+    if (!(e.z >> 31) && b > e.y) *gref<NT>(P, x, g) = make_uint4(e.x, b, e.z, 0u);
     return;
   }
-  if ((g = ghost_alloc<NT>(P, x)) < GMAX) P.gst[gidx<NT>(P, x, g)] = make_uint4((uint32_t)s, b, ghost_until<NT>(P, x), 0u);
+  if ((g = ghost_alloc<NT>(P, x)) < GMAX) *gref<NT>(P, x, g) = make_uint4((uint32_t)s, b, ghost_until<NT>(P, x), 0u);
 }
 // HandleP3 on a slot below execute: the entry exists and is committed (paxos.go:326-331)
 template <int NT>
@@ -173,11 +255,11 @@ __device__ __forceinline__ void ghost_commit(const Params& P, Rep<NT>& x, int32_
   uint4 e;
   uint32_t g = ghost_find<NT>(P, x, s, e);
   if (g < GMAX) {
-    P.gst[gidx<NT>(P, x, g)] = make_uint4(e.x, e.y, e.z | 0x80000000u, 0u);
+    *gref<NT>(P, x, g) = make_uint4(e.x, e.y, e.z | 0x80000000u, 0u);
     return;
   }
   if ((g = ghost_alloc<NT>(P, x)) < GMAX)
-    P.gst[gidx<NT>(P, x, g)] = make_uint4((uint32_t)s, 0u, ghost_until<NT>(P, x) | 0x80000000u, 0u);
+    *gref<NT>(P, x, g) = make_uint4((uint32_t)s, 0u, ghost_until<NT>(P, x) | 0x80000000u, 0u);
 }
 // HandleP2b (paxos.go:270-310) for a slot below execute
 template <int NT>
@@ -283,22 +365,25 @@ static __device__ __noinline__ void agree_arrive(unsigned long long* a, uint32_t
 template <int NT>
 __device__ __forceinline__ void kv_exec(const Params& P, Rep<NT>& x, uint32_t cmd) {
   if (!wl_write(P, x.kc, cmd)) return;
-  P.kv_val[((size_t)wl_key(P, x.kc, cmd) * nrep<NT>(P) + x.r) * P.C + x.c] = cmd;
+  // a per-key instance (HBM log: WPaxos, M2Paxos, KPaxos) only executes commands of its own key
+  const uint32_t key = hbm_log(x) ? x.key : wl_key(P, x.kc, cmd);
+  P.kv_val[((size_t)key * nrep<NT>(P) + x.r) * P.C + x.c] = cmd;
   x.kvver++;
 }
 
 template <int NT>
 __device__ __forceinline__ void paxos_exec(const Params& P, Rep<NT>& x) {     // paxos.go:345-369
   for (;;) {
+    if (hbm_log(x) && x.execute > x.slot) break;                   // entries exist only up to p.slot (saves an HBM read)
     const uint32_t i = eidx<NT>(P, x, x.execute);
-    const uint32_t c = x.l_b[i];
+    const uint32_t c = eb(x, i);
     if ((c & (EF_EXISTS | EF_COMMIT)) != (EF_EXISTS | EF_COMMIT)) break;
     if (x.iflags & PAXISIM_F_WOVF) x.flags |= PAXISIM_F_UNFAITHFUL;
     const uint32_t cmd = c & CMD_MASK;
     if (c & (EF_REQSELF | EF_REQEXT)) request_reply<NT>(P, x, ereq<NT>(P, x, i, c), cmd);
     x.digest = mix64(x.digest ^ (((uint64_t)(uint32_t)x.execute << 32) | cmd));
     if (P.kv) kv_exec<NT>(P, x, cmd);                              // p.Execute(e.command), paxos.go:352
-    x.l_b[i] = 0u;                                                 // delete(p.log, execute)
+    set_b(x, i, 0u);                                               // delete(p.log, execute)
     x.execute++;
     if ((uint32_t)x.execute % CKI == 0) {
       const uint32_t k = ((uint32_t)x.execute / CKI) % CKR;
@@ -326,7 +411,7 @@ __device__ __forceinline__ void paxos_handle_p1a(const Params& P, Rep<NT>& x, ui
   if (hi > x.execute + (int32_t)P.W - 1) hi = x.execute + (int32_t)P.W - 1;
   uint32_t n = 0;
   for (int32_t s = x.execute; s <= hi; s++) {
-    const uint32_t c = x.l_b[eidx<NT>(P, x, s)];
+    const uint32_t c = eb(x, eidx<NT>(P, x, s));
     n += (c & EF_EXISTS) && !(c & EF_COMMIT);
   }
   uint32_t ri;
@@ -382,11 +467,9 @@ __device__ __forceinline__ void paxos_handle_p1b(const Params& P, Rep<NT>& x, ui
       if (hi > x.execute + (int32_t)P.W - 1) hi = x.execute + (int32_t)P.W - 1;
       for (int32_t s = x.execute; s <= hi; s++) {
         const uint32_t i = eidx<NT>(P, x, s);
-        const uint32_t c = x.l_b[i];
+        const uint32_t c = eb(x, i);
         if (!(c & EF_EXISTS) || (c & EF_COMMIT)) continue;                   // nil gap (G5)
-        x.l_a[i] = x.ballot;
-        x.l_b[i] = c | EF_QUORUM;
-        x.l_c[i] = 1u << x.r;
+        eput<NT>(x, i, Ent{x.ballot, c | EF_QUORUM, 1u << x.r});
         post_broadcast<NT>(P, x, PAXISIM_MSG_P2A | x.ktag, x.ballot, (uint32_t)s, c & CMD_MASK);
       }
       const uint32_t np = x.npend;
@@ -414,8 +497,8 @@ __device__ __forceinline__ void paxos_handle_p2a(const Params& P, Rep<NT>& x, ui
           }
           e.c = eset_cmd<NT>(P, x, i, e.c, mcid);
           e.b = mb;
-          x.l_a[i] = e.b;
-          x.l_b[i] = e.c;
+          set_a(x, i, e.b);
+          set_b(x, i, e.c);
         }
       } else {
         eput<NT>(x, i, Ent{mb, mcid | EF_EXISTS, 0u});
@@ -438,23 +521,23 @@ __device__ __forceinline__ void paxos_handle_p2b(const Params& P, Rep<NT>& x, ui
     return;
   }
   const uint32_t i = eidx<NT>(P, x, ms);
-  const uint32_t c = x.l_b[i];
-  const uint32_t eb = x.l_a[i];
-  if (!(c & EF_EXISTS) || mb < eb || (c & EF_COMMIT)) return;
+  const uint32_t c = eb(x, i);
+  const uint32_t eb0 = ea(x, i);
+  if (!(c & EF_EXISTS) || mb < eb0 || (c & EF_COMMIT)) return;
   if (mb > x.ballot) {
     x.ballot = mb;
     x.active = 0;
   }
-  if (bal_id(mb) == x.r && mb == eb) {
+  if (bal_id(mb) == x.r && mb == eb0) {
     if (!(c & EF_QUORUM)) {                                                   // nil quorum: Go panics
       x.flags |= PAXISIM_F_POISON;
       x.stop = true;
       return;
     }
-    const uint32_t ack = x.l_c[i] | (1u << src);
-    x.l_c[i] = ack;
+    const uint32_t ack = ec(x, i) | (1u << src);
+    set_c(x, i, ack);
     if (quorum_ok(P, P.q2, ack)) {
-      x.l_b[i] = c | EF_COMMIT;
+      set_b(x, i, c | EF_COMMIT);
       x.commits++;
       post_broadcast<NT>(P, x, PAXISIM_MSG_P3 | x.ktag, mb, (uint32_t)ms, c & CMD_MASK);
       if (P.rwc) {
@@ -474,7 +557,7 @@ __device__ __forceinline__ void paxos_handle_p3(const Params& P, Rep<NT>& x, uin
   if (ms > x.slot) x.slot = ms;
   if (in_window<NT>(P, x, ms)) {
     const uint32_t i = eidx<NT>(P, x, ms);
-    uint32_t c = x.l_b[i];
+    uint32_t c = eb(x, i);
     if (c & EF_EXISTS) {
       if ((c & CMD_MASK) != mcid && (c & (EF_REQSELF | EF_REQEXT))) {
         node_forward<NT>(P, x, bal_id(mb), ereq<NT>(P, x, i, c));
@@ -482,11 +565,11 @@ __device__ __forceinline__ void paxos_handle_p3(const Params& P, Rep<NT>& x, uin
       }
     } else {
       c = EF_EXISTS;                                                          // &entry{} (G6)
-      x.l_a[i] = 0u;
-      x.l_c[i] = 0u;
+      set_a(x, i, 0u);
+      set_c(x, i, 0u);
     }
     c = eset_cmd<NT>(P, x, i, c, mcid) | EF_COMMIT;
-    x.l_b[i] = c;
+    set_b(x, i, c);
     if (P.rwc) {
       if (c & (EF_REQSELF | EF_REQEXT)) {
         const uint32_t q = ereq<NT>(P, x, i, c);
@@ -558,14 +641,14 @@ struct PaxosProto {
     if (!in_window<NT>(P, x, ms))
       return ms < x.execute ? !(x.iflags & PAXISIM_F_GHOST) : !(x.iflags & PAXISIM_F_WOVF);
     const uint32_t i = eidx<NT>(P, x, ms);
-    const uint32_t c = x.l_b[i];
-    const uint32_t eb = x.l_a[i];
-    if (!(c & EF_EXISTS) || mb < eb || (c & EF_COMMIT)) return true;
-    if (bal_id(mb) == x.r && mb == eb) {
+    const uint32_t c = eb(x, i);
+    const uint32_t eb0 = ea(x, i);
+    if (!(c & EF_EXISTS) || mb < eb0 || (c & EF_COMMIT)) return true;
+    if (bal_id(mb) == x.r && mb == eb0) {
       if (!(c & EF_QUORUM)) return false;                 // nil quorum: the full handler poisons
-      const uint32_t ack = x.l_c[i] | (1u << src);
+      const uint32_t ack = ec(x, i) | (1u << src);
       if (quorum_ok(P, P.q2, ack)) return false;          // commit: the full handler
-      x.l_c[i] = ack;
+      set_c(x, i, ack);
     }
     if (mb > x.ballot) {
       x.ballot = mb;
@@ -578,13 +661,13 @@ struct PaxosProto {
   __device__ static __forceinline__ void dispatch(const Params& P, Rep<NT>& x, uint32_t src, const uint4& m,
                                                   uint32_t ri) {
     switch (hdr_type(m.x)) {
-      case PAXISIM_MSG_REQUEST: dv_inc<NT>(x, PAXISIM_MSG_REQUEST); handle_request<NT>(P, x, mkreq(m.w, src)); break;
-      case PAXISIM_MSG_REPLY: dv_inc<NT>(x, PAXISIM_MSG_REPLY); handle_reply<NT>(P, x, m.w); break;
-      case PAXISIM_MSG_P1A: dv_inc<NT>(x, PAXISIM_MSG_P1A); paxos_handle_p1a<NT>(P, x, m.y); break;
-      case PAXISIM_MSG_P1B: dv_inc<NT>(x, PAXISIM_MSG_P1B); paxos_handle_p1b<NT>(P, x, src, m.y, ri, hdr_n(m.x)); break;
-      case PAXISIM_MSG_P2A: dv_inc<NT>(x, PAXISIM_MSG_P2A); paxos_handle_p2a<NT>(P, x, m.y, (int32_t)m.z, m.w); break;
-      case PAXISIM_MSG_P2B: dv_inc<NT>(x, PAXISIM_MSG_P2B); paxos_handle_p2b<NT>(P, x, src, m.y, (int32_t)m.z); break;
-      case PAXISIM_MSG_P3: dv_inc<NT>(x, PAXISIM_MSG_P3); paxos_handle_p3<NT>(P, x, m.y, (int32_t)m.z, m.w); break;
+      case PAXISIM_MSG_REQUEST: { PXS_CASE_T0 dv_inc<NT>(x, PAXISIM_MSG_REQUEST); handle_request<NT>(P, x, mkreq(m.w, src)); PXS_CASE_T1(PAXISIM_MSG_REQUEST) } break;
+      case PAXISIM_MSG_REPLY: { PXS_CASE_T0 dv_inc<NT>(x, PAXISIM_MSG_REPLY); handle_reply<NT>(P, x, m.w); PXS_CASE_T1(PAXISIM_MSG_REPLY) } break;
+      case PAXISIM_MSG_P1A: { PXS_CASE_T0 dv_inc<NT>(x, PAXISIM_MSG_P1A); paxos_handle_p1a<NT>(P, x, m.y); PXS_CASE_T1(PAXISIM_MSG_P1A) } break;
+      case PAXISIM_MSG_P1B: { PXS_CASE_T0 dv_inc<NT>(x, PAXISIM_MSG_P1B); paxos_handle_p1b<NT>(P, x, src, m.y, ri, hdr_n(m.x)); PXS_CASE_T1(PAXISIM_MSG_P1B) } break;
+      case PAXISIM_MSG_P2A: { PXS_CASE_T0 dv_inc<NT>(x, PAXISIM_MSG_P2A); paxos_handle_p2a<NT>(P, x, m.y, (int32_t)m.z, m.w); PXS_CASE_T1(PAXISIM_MSG_P2A) } break;
+      case PAXISIM_MSG_P2B: { PXS_CASE_T0 dv_inc<NT>(x, PAXISIM_MSG_P2B); paxos_handle_p2b<NT>(P, x, src, m.y, (int32_t)m.z); PXS_CASE_T1(PAXISIM_MSG_P2B) } break;
+      case PAXISIM_MSG_P3: { PXS_CASE_T0 dv_inc<NT>(x, PAXISIM_MSG_P3); paxos_handle_p3<NT>(P, x, m.y, (int32_t)m.z, m.w); PXS_CASE_T1(PAXISIM_MSG_P3) } break;
       default: break;
     }
   }

@@ -31,6 +31,8 @@ struct Rep {
   uint32_t key, exists, pol;            // WPaxos: key, r.paxi[key] != nil, policy last | hits << 8
   uint32_t iflags;                      // WOVF / GHOST of the bound instance
   uint32_t e0, es;                      // log entry i of slot s: e0 + (s & (W-1)) * es
+  uint4 ce;                             // HBM-resident window (es = 4): entry at word ci, cached (paxos_kernel.h)
+  uint32_t ci;
   uint32_t* reqx;                       // request side table, indexed like the log
   uint32_t* pend;                       // pending request k at pend[k * pstride]
   uint32_t pstride;
@@ -163,10 +165,40 @@ __device__ __forceinline__ void broadcast1(const Params& P, Rep<NT>& x, uint32_t
 // and emission walks destinations in index order, so every link sees its
 // records in exactly the order the handlers issued them.
 // ---------------------------------------------------------------------------
+#ifndef PXS_FLUSH1_9
+#define PXS_FLUSH1_9 1   // 9-replica WPaxos kernel: one pass per destination (no 2 x 9 transient registers)
+#endif
 template <int NT>
 __device__ __forceinline__ void intent_flush(const Params& P, Rep<NT>& x) {
   if (!x.im) return;
   constexpr uint32_t NU = NT ? (uint32_t)NT : (uint32_t)PAXISIM_MAX_N;
+  if (NT == 9 && PXS_FLUSH1_9 && x.es == 4u) {   // (the HBM-log kernel: A/B r2 +, the LDS-window one -)
+#pragma unroll
+    for (uint32_t d = 0; d < NU; d++) {
+      if (!((x.im >> d) & 1u)) continue;
+      const uint32_t seq = x.send_seq++;
+      x.sent++;
+      if ((x.dmask >> d) & 1u) { x.dropped++; continue; }
+      if ((x.fmask >> d) & 1u) {
+        uint32_t p = 0;
+        scripted(P, PAXISIM_FAULT_FLAKY, x.gid, x.r, d, x.t, &p);
+        if (ppm_hit(draw(x.hs, tag(PUR_FLAKY, x.r, seq)), p)) { x.dropped++; continue; }
+      }
+      uint32_t b = x.b0 + 1u + (uint32_t)((x.dly >> (4u * d)) & 15u);
+      if (b >= P.D) b -= P.D;
+      const uint32_t box = (b * NU + d) * P.NS + x.r;
+      const uint32_t k = x.l_cnt[(box << 6) | x.lane];
+      if (k + 1u > P.M) {
+        x.flags |= PAXISIM_F_MBOX_OVF | PAXISIM_F_UNFAITHFUL;
+        x.dropped++;
+        continue;
+      }
+      x.l_cnt[(box << 6) | x.lane] = (uint8_t)(k + 1u);
+      x.rec[((box * P.M + k) << 6) | x.lane] = make_uint4(x.iw0, x.iw1, x.iw2, x.iw3);
+    }
+    x.im = 0;
+    return;
+  }
   // pass 1: the bucket count of every destination (independent LDS reads:
   // each destination has its own box, so reading them up front is exact)
   uint32_t box[NU], k[NU];
@@ -367,13 +399,45 @@ __device__ __forceinline__ void fault_process(const Params& P, Rep<NT>& x, uint3
 // ---------------------------------------------------------------------------
 // One replica, one step
 // ---------------------------------------------------------------------------
+// Records left per source in the merge.  9-replica kernels pack them into
+// bytes (four sources a register: counts are at most M <= 255), which frees
+// seven registers across the merge loop; the others keep one a source.
+#ifndef PXS_PACKREM9
+#define PXS_PACKREM9 1
+#endif
+template <uint32_t NS, bool PACK>
+struct RemT {
+  uint32_t v[NS];
+  __device__ __forceinline__ void clear() {
+#pragma unroll
+    for (uint32_t s = 0; s < NS; s++) v[s] = 0;
+  }
+  __device__ __forceinline__ uint32_t get(uint32_t s) const { return opaque(v[s]); }   // s: a constant
+  __device__ __forceinline__ void put(uint32_t s, uint32_t n) { v[s] = n; }           // after clear()
+  __device__ __forceinline__ void sub(uint32_t src, uint32_t n) {
+#pragma unroll
+    for (uint32_t s = 0; s < NS; s++) v[s] = opaque(v[s]) - (s == src ? n : 0u);
+  }
+};
+template <uint32_t NS>
+struct RemT<NS, true> {
+  static constexpr uint32_t NW = (NS + 3u) / 4u;
+  uint32_t w[NW];
+  __device__ __forceinline__ void clear() {
+#pragma unroll
+    for (uint32_t k = 0; k < NW; k++) w[k] = 0;
+  }
+  __device__ __forceinline__ uint32_t get(uint32_t s) const { return (opaque(w[s >> 2]) >> ((s & 3u) * 8u)) & 0xFFu; }
+  __device__ __forceinline__ void put(uint32_t s, uint32_t n) { w[s >> 2] |= n << ((s & 3u) * 8u); }
+  __device__ __forceinline__ void sub(uint32_t src, uint32_t n) {   // never borrows: n <= the count
+    const uint32_t d = n << ((src & 3u) * 8u);
+#pragma unroll
+    for (uint32_t k = 0; k < NW; k++) w[k] = opaque(w[k]) - ((src >> 2) == k ? d : 0u);
+  }
+};
+
 #ifdef PXS_STAMPS
 struct Stamps { unsigned long long setup, loop, barrier, trips, msgs, steps, pick, disp, wait, flush, stage, tail; };
-__device__ __forceinline__ unsigned long long stamp() {
-  unsigned long long t;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  return t;
-}
 #endif
 
 template <int NT, class Proto, bool STAGED>
@@ -409,12 +473,13 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
   // per source: records left (rem) and the step's initial count, packed in
   // bytes (c0w), so a source's FIFO position is c0 - rem without a register each
   constexpr uint32_t NCW = (NSMAX + 3u) / 4u;
-  uint32_t rem[NSMAX], c0w[NCW], total = 0;
+  RemT<NSMAX, NT == 9 && PXS_PACKREM9> rem;
+  uint32_t c0w[NCW], total = 0;
+  rem.clear();
 #pragma unroll
   for (uint32_t k = 0; k < NCW; k++) c0w[k] = 0;
 #pragma unroll
   for (uint32_t s = 0; s < NSMAX; s++) {
-    rem[s] = 0;
     if (s < NS) {
       uint32_t n = x.l_cnt[((box0 + s) << 6) | x.lane];
       if (x.crashed && s < N && n) {                    // socket.Recv discards (socket.go:111-118)
@@ -425,7 +490,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
         }
         n = 0;
       }
-      rem[s] = n;
+      rem.put(s, n);
       c0w[s >> 2] |= n << ((s & 3u) * 8u);
       total += n;
     }
@@ -445,7 +510,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
   uint32_t u = 0, i = 0, src = 0, ri = 0;
   uint4 m = make_uint4(0u, 0u, 0u, 0u);
   // pick idx: the source of the idx-th message, given the remaining counts
-  auto pick_from = [&](uint32_t idx, uint32_t tot, const uint32_t (&rm)[NSMAX], uint32_t& uu, uint32_t& psrc,
+  auto pick_from = [&](uint32_t idx, uint32_t tot, const decltype(rem)& rm, uint32_t& uu, uint32_t& psrc,
                        uint32_t& pri) {
     if (!(idx & 1u)) uu = draw(x.hs, tag(PUR_ORDER, x.r, idx >> 1));
     uint32_t pk = (((idx & 1u) ? (uu >> 16) : (uu & 0xFFFFu)) * tot) >> 16;
@@ -454,7 +519,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
     uint32_t p0 = 0;
 #pragma unroll
     for (uint32_t s = 0; s < NSMAX; s++) {
-      const uint32_t rs = opaque(rm[s]);
+      const uint32_t rs = rm.get(s);
       const bool here = !found && pk < rs;
       if (here) { psrc = s; p0 = ((c0w[s >> 2] >> ((s & 3u) * 8u)) & 0xFFu) - rs; found = true; }
       else if (!found) pk -= rs;
@@ -478,16 +543,14 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
   if constexpr (STAGED) {
     const uint32_t sbase = __builtin_amdgcn_readfirstlane(P.off_stage + x.r * P.J * 1024u);
     stage = reinterpret_cast<const uint4*>(x.l_cnt - P.img.off_cnt + sbase) + x.lane;
-    uint32_t srem[NSMAX], su = 0;
-#pragma unroll
-    for (uint32_t s = 0; s < NSMAX; s++) srem[s] = rem[s];
+    auto srem = rem;
+    uint32_t su = 0;
     for (uint32_t j = 0; j < P.J; j++) {
       if (!__ballot(j < total)) break;
       if (j < total) {
         uint32_t ssrc, sri;
         pick_from(j, total - j, srem, su, ssrc, sri);
-#pragma unroll
-        for (uint32_t s = 0; s < NSMAX; s++) srem[s] = opaque(srem[s]) - (s == ssrc ? 1u : 0u);
+        srem.sub(ssrc, 1u);
         __builtin_amdgcn_global_load_lds(
             (__attribute__((address_space(1))) void*)(x.rec + sri),
             (__attribute__((address_space(3))) void*)((__attribute__((address_space(3))) uint8_t*)(x.l_cnt -
@@ -517,7 +580,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
     uint32_t p0 = 0;
 #pragma unroll
     for (uint32_t s = 0; s < NSMAX; s++) {
-      const uint32_t rs = opaque(rem[s]) - (s == skip ? 1u : 0u);
+      const uint32_t rs = rem.get(s) - (s == skip ? 1u : 0u);
       const bool here = !found && pk < rs;
       if (here) { psrc = s; p0 = ((c0w[s >> 2] >> ((s & 3u) * 8u)) & 0xFFu) - rs; found = true; }
       else if (!found) pk -= rs;
@@ -541,8 +604,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
     const unsigned long long w0 = stamp();
 #endif
     const uint32_t len = rec_len(m.x);
-#pragma unroll
-    for (uint32_t s = 0; s < NSMAX; s++) rem[s] = opaque(rem[s]) - (s == src ? len : 0u);
+    rem.sub(src, len);
     total -= len;
     if (len > 1u && jv > i + 1u) jv = i + 1u;          // later picks differ from the staged ones
 #ifdef PXS_STAMPS
@@ -603,8 +665,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
       for (int k = 0; k < PXS_ABSORB_MAX; k++) {
         if (!(total && !x.stop && nsrc != N && Proto::template absorb<NT>(P, x, nsrc, nm))) break;
         dv_inc<NT>(x, hdr_type(nm.x));
-#pragma unroll
-        for (uint32_t s = 0; s < NSMAX; s++) rem[s] = opaque(rem[s]) - (s == nsrc ? 1u : 0u);
+        rem.sub(nsrc, 1u);
         total -= 1u;
         i++;
         if constexpr (PF2) {                            // the after-next becomes the next
@@ -732,6 +793,9 @@ __global__ void __launch_bounds__(max_threads<NT>(), min_waves<NT>()) sim_steps(
   x.l_cnt = L + P.img.off_cnt;
   x.rec = P.rec + (size_t)blk * P.rec_per_block;
   const bool live = x.c < bound && x.r < N;
+  // the log layout is a constant of the instance (paxos_kernel.h: hbm_log)
+  x.es = Proto::kind == PAXISIM_WPAXOS ? 4u : LANES;
+  x.ci = ~0u;
   if (live) {
     const size_t i = rc(P, x.r, x.c);
     x.kc = P.kc[x.c];
@@ -776,7 +840,7 @@ __global__ void __launch_bounds__(max_threads<NT>(), min_waves<NT>()) sim_steps(
   }
 #ifdef PXS_STAMPS
   if (x.lane == 0 && P.dbg) {
-    unsigned long long* d = &P.dbg[((size_t)blk * 16 + x.r) * 16];
+    unsigned long long* d = &P.dbg[((size_t)blk * 16 + x.r) * DBG_PER];
     atomicAdd(&d[0], st.setup); atomicAdd(&d[1], st.loop); atomicAdd(&d[2], st.barrier);
     atomicAdd(&d[3], st.trips); atomicAdd(&d[4], st.msgs); atomicAdd(&d[5], st.steps);
     atomicAdd(&d[6], st.pick); atomicAdd(&d[7], st.disp);

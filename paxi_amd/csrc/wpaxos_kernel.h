@@ -62,6 +62,7 @@ __device__ __forceinline__ void wp_bind(const Params& P, Rep<NT>& x, uint32_t ke
   x.l_c = lb + 2;
   x.reqx = lb + 3;
   x.pend = P.wpend + si * PMAX;
+  x.ci = ~0u;                        // the entry cache belongs to the bound window
 }
 template <int NT>
 __device__ __forceinline__ void wp_unbind(const Params& P, const Rep<NT>& x) {
@@ -228,9 +229,11 @@ struct WPaxosProto {
   }
   template <int NT>
   __device__ static __forceinline__ void client_request(const Params& P, Rep<NT>& x, uint32_t cid) {
+    PXS_CASE_T0
     wp_bind<NT>(P, x, wl_key(P, x.kc, cid));
     wp_handle_request<NT>(P, x, mkreq(cid, PAXISIM_CLIENT_SRC));
     wp_unbind<NT>(P, x);
+    PXS_CASE_T1(0)
   }
   // registrations replica.go:25-32
   template <int NT>
@@ -238,46 +241,73 @@ struct WPaxosProto {
                                                   uint32_t ri) {
     const uint32_t type = hdr_type(m.x);
     if (type == PAXISIM_MSG_REPLY) {                                   // node.recv (node.go:83-90)
+      PXS_CASE_T0
       dv_inc<NT>(x, PAXISIM_MSG_REPLY);
       handle_reply<NT>(P, x, m.w);
+      PXS_CASE_T1(PAXISIM_MSG_REPLY)
       return;
     }
-    wp_bind<NT>(P, x, type == PAXISIM_MSG_REQUEST ? wl_key(P, x.kc, m.w) : hdr_key(m.x));
+    {
+      PXS_CASE_T0
+      wp_bind<NT>(P, x, type == PAXISIM_MSG_REQUEST ? wl_key(P, x.kc, m.w) : hdr_key(m.x));
+      // the entry of the message's slot (P2a / P2b / P3; harmless for the
+      // others: any slot indexes the window): its load goes out with the bind's
+      ecache<NT>(x, (m.z & (P.W - 1u)) * 4u);
+      PXS_CASE_T1(14)
+    }
     switch (type) {
       case PAXISIM_MSG_REQUEST:
+        { PXS_CASE_T0
         dv_inc<NT>(x, PAXISIM_MSG_REQUEST);
         wp_handle_request<NT>(P, x, mkreq(m.w, src));
+        PXS_CASE_T1(PAXISIM_MSG_REQUEST) }
         break;
       case PAXISIM_MSG_P1A:                                            // handlePrepare 72-76
+        { PXS_CASE_T0
         dv_inc<NT>(x, PAXISIM_MSG_P1A);
         wp_create<NT>(P, x);
         paxos_handle_p1a<NT>(P, x, m.y);
+        PXS_CASE_T1(PAXISIM_MSG_P1A) }
         break;
       case PAXISIM_MSG_P1B:                                            // handlePromise 78-82
+        { PXS_CASE_T0
         dv_inc<NT>(x, PAXISIM_MSG_P1B);
         if (wp_get<NT>(x)) paxos_handle_p1b<NT>(P, x, src, m.y, ri, hdr_n(m.x));
+        PXS_CASE_T1(PAXISIM_MSG_P1B) }
         break;
       case PAXISIM_MSG_P2A:                                            // handleAccept 84-88
+        { PXS_CASE_T0
         dv_inc<NT>(x, PAXISIM_MSG_P2A);
         wp_create<NT>(P, x);
         paxos_handle_p2a<NT>(P, x, m.y, (int32_t)m.z, m.w);
+        PXS_CASE_T1(PAXISIM_MSG_P2A) }
         break;
       case PAXISIM_MSG_P2B:                                            // handleAccepted 90-93
+        { PXS_CASE_T0
         dv_inc<NT>(x, PAXISIM_MSG_P2B);
         if (wp_get<NT>(x)) paxos_handle_p2b<NT>(P, x, src, m.y, (int32_t)m.z);
+        PXS_CASE_T1(PAXISIM_MSG_P2B) }
         break;
       case PAXISIM_MSG_P3:                                             // handleCommit 95-99
+        { PXS_CASE_T0
         dv_inc<NT>(x, PAXISIM_MSG_P3);
         wp_create<NT>(P, x);
         paxos_handle_p3<NT>(P, x, m.y, (int32_t)m.z, m.w);
+        PXS_CASE_T1(PAXISIM_MSG_P3) }
         break;
       case PAXISIM_MSG_LEADERCHG:                                      // handleLeaderChange 101-108
+        { PXS_CASE_T0
         dv_inc<NT>(x, PAXISIM_MSG_LEADERCHG);
         if (wp_get<NT>(x) && m.y == x.ballot && m.z == x.r) paxos_p1a<NT>(P, x);
+        PXS_CASE_T1(PAXISIM_MSG_LEADERCHG) }
         break;
       default: break;
     }
-    wp_unbind<NT>(P, x);
+    {
+      PXS_CASE_T0
+      wp_unbind<NT>(P, x);
+      PXS_CASE_T1(15)
+    }
   }
 };
 

@@ -64,6 +64,8 @@ def load_library():
     L.paxisim_dist_stats.argtypes = [C.c_void_p, P(abi.Stats), P(C.c_double)]
     L.paxisim_dist_destroy.restype = C.c_int
     L.paxisim_dist_destroy.argtypes = [C.c_void_p]
+    L.paxisim_commands.restype = C.c_int
+    L.paxisim_commands.argtypes = [C.c_void_p, C.c_uint64, P(C.c_uint32), C.c_uint32, P(C.c_uint32), P(C.c_uint32)]
     if L.paxisim_abi_version() != abi.ABI_VERSION:
         raise PaxisimError("ABI version mismatch between paxi_amd/abi.py and libpaxisim.so")
     _lib = L
@@ -76,12 +78,23 @@ EXPORTED = ["paxisim_abi_version", "paxisim_last_error", "paxisim_create", "paxi
             "paxisim_linearizable", "paxisim_history", "paxisim_occupancy", "paxisim_inject", "paxisim_read_log",
             "paxisim_history_load", "paxisim_active_clusters", "paxisim_dist_init", "paxisim_dist_unique_id",
             "paxisim_dist_init_rank", "paxisim_dist_allreduce", "paxisim_dist_stats", "paxisim_dist_destroy",
-            "paxisim_read_kv"]
+            "paxisim_read_kv", "paxisim_read_inbox", "paxisim_deliver", "paxisim_commands"]
 
 
 def _check(rc):
     if rc != 0:
         raise PaxisimError(f"paxisim error {rc}: {load_library().paxisim_last_error().decode()}")
+
+
+def _read_inbox(fn, h, cluster, replica, check):
+    n = C.c_uint32()
+    cap = 256
+    while True:
+        arr = (abi.InboxRecord * cap)()
+        check(fn(h, cluster, replica, arr, cap, C.byref(n)))
+        if n.value <= cap:
+            return [arr[i].as_tuple() for i in range(n.value)]
+        cap = n.value
 
 
 class Simulation:
@@ -132,6 +145,24 @@ class Simulation:
     def inject(self, cluster, replica, cid):
         """A client request for command `cid` at `replica` in the next step (http.go:99)."""
         _check(load_library().paxisim_inject(self.h, cluster, replica, cid))
+
+    def read_inbox(self, cluster, replica):
+        """Records replica `replica` receives at the next step, by source (paxisim_read_inbox)."""
+        return _read_inbox(load_library().paxisim_read_inbox, self.h, cluster, replica, _check)
+
+    def commands(self, cluster, cids):
+        """[(key index, is_write)] of command ids of a cluster (paxisim_commands)."""
+        n = len(cids)
+        a = (C.c_uint32 * max(1, n))(*cids)
+        k, w = (C.c_uint32 * max(1, n))(), (C.c_uint32 * max(1, n))()
+        _check(load_library().paxisim_commands(self.h, cluster, a, n, k, w))
+        return [(k[i], bool(w[i])) for i in range(n)]
+
+    def deliver(self, cluster, replica, src, recs):
+        """Append records (src, hdr, ballot, slot, cid) to the replica's next-step
+        inbox from source `src` (paxisim_deliver; a record's own src is ignored)."""
+        arr = (abi.InboxRecord * max(1, len(recs)))(*[abi.InboxRecord(src, *r[-4:]) for r in recs])
+        _check(load_library().paxisim_deliver(self.h, cluster, replica, src, arr, len(recs)))
 
     def read_log(self, cluster, replica, slot_lo, n, key=0):
         """paxos.go entries of slots [slot_lo, slot_lo+n) of one instance (paxisim_read_log)."""

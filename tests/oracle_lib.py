@@ -88,6 +88,19 @@ class OracleSim:
     def inject(self, cluster, replica, cid):
         _check(lib().oracle_inject(self.h, cluster, replica, cid))
 
+    def commands(self, cluster, cids):
+        return [self.command(cluster, c) for c in cids]
+
+    def read_inbox(self, cluster, replica):
+        from paxi_amd.sim import _read_inbox
+        lib().oracle_read_inbox.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.POINTER(abi.InboxRecord),
+                                            C.c_uint32, C.POINTER(C.c_uint32)]
+        return _read_inbox(lib().oracle_read_inbox, self.h, cluster, replica, _check)
+
+    def deliver(self, cluster, replica, src, recs):
+        arr = (abi.InboxRecord * max(1, len(recs)))(*[abi.InboxRecord(src, *r[-4:]) for r in recs])
+        _check(lib().oracle_deliver(self.h, cluster, replica, src, arr, len(recs)))
+
     def read_log(self, cluster, replica, slot_lo, n, key=0):
         arr = (abi.LogEntry * max(1, n))()
         _check(lib().oracle_read_log(self.h, cluster, replica, key, slot_lo, n, arr))
