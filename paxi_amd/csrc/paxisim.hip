@@ -265,7 +265,7 @@ __global__ void gather_inst_kernel(Params P, uint64_t lo, uint64_t n, paxisim_in
     s.npending = b.x;
     s.digest = (uint64_t)b.y | ((uint64_t)b.z << 32);
     s.policy_last = b.w & 0xFFu;
-    s.policy_hits = b.w >> 8;
+    s.policy_hits = (b.w >> 8) & 0xFFu;
     if (P.policy == PAXISIM_POLICY_MAJORITY) {
       const uint4 h0 = P.wpx[3 * si], h1 = P.wpx[3 * si + 1], m = P.wpx[3 * si + 2];
       const uint32_t w[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
@@ -851,6 +851,13 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     if (P.start_step[w]) P.late_workers |= 1u << w;
   }
 
+  P.keys_magic = 0xFFFFFFFFu / P.keys;
+  for (uint32_t w = 0; w < PAXISIM_MAX_WORKERS; w++) {
+    const uint32_t z = w < P.WK ? P.zone_of[P.target[w] < N ? P.target[w] : 0u] : 0u;
+    P.wzone[w] = z;
+    P.wnk[w] = z < P.keys ? (P.keys - z + P.Z - 1u) / P.Z : 0u;
+    P.wnk_magic[w] = P.wnk[w] ? 0xFFFFFFFFu / P.wnk[w] : 0u;
+  }
   P.img = proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D);
   {
     // Cluster groups per workgroup (sim_core.h): as many 64-cluster tiles as

@@ -98,6 +98,11 @@ struct Params {
   uint32_t target[PAXISIM_MAX_WORKERS];
   uint32_t start_step[PAXISIM_MAX_WORKERS];   // first request of worker w at this step
   uint32_t late_workers;                      // mask of workers with start_step > 0
+  // workload keys (sim_core.h wl_key), per worker w: zone z of its target, the
+  // count nk of that zone's keys {k = z mod Z} and floor((2^32-1)/nk); and
+  // floor((2^32-1)/keys): (x % d) as a multiply-high and one correction
+  uint32_t wzone[PAXISIM_MAX_WORKERS], wnk[PAXISIM_MAX_WORKERS], wnk_magic[PAXISIM_MAX_WORKERS];
+  uint32_t keys_magic;
   Image img;
   uint32_t J, off_stage;   // LDS stage: J staged picks per replica at LDS byte off_stage ([r][J][64] x 16 B)
   uint32_t lds_bytes;      // LDS per cluster group (16-B multiple): the image + the stage

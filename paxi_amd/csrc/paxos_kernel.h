@@ -59,9 +59,16 @@ __device__ __forceinline__ void set_a(Rep<NT>& x, uint32_t i, uint32_t v) {
   if (hbm_log(x)) { x.l_a[i] = v; if (x.ci == i) x.ce.x = v; return; }
   x.l_a[i] = v;
 }
+// committed-entry bits of an HBM-resident window: exec() stops at the first
+// clear bit without reading the entry (W <= 16; wider windows read it)
+template <int NT>
+__device__ __forceinline__ void cm_note(Rep<NT>& x, uint32_t i, uint32_t c) {
+  const uint32_t bit = 1u << ((i >> 2) & 31u);
+  x.cmask = (c & EF_COMMIT) ? (x.cmask | bit) : (x.cmask & ~bit);
+}
 template <int NT>
 __device__ __forceinline__ void set_b(Rep<NT>& x, uint32_t i, uint32_t v) {
-  if (hbm_log(x)) { x.l_a[i + 1u] = v; if (x.ci == i) x.ce.y = v; return; }
+  if (hbm_log(x)) { x.l_a[i + 1u] = v; if (x.ci == i) x.ce.y = v; cm_note(x, i, v); return; }
   x.l_b[i] = v;
 }
 template <int NT>
@@ -78,6 +85,7 @@ __device__ __forceinline__ void eput(Rep<NT>& x, uint32_t i, const Ent& e) {
     *reinterpret_cast<uint2*>(q) = make_uint2(e.b, e.c);
     q[2] = e.a;
     if (x.ci == i) { x.ce.x = e.b; x.ce.y = e.c; x.ce.z = e.a; }
+    cm_note(x, i, e.c);
     return;
   }
   x.l_a[i] = e.b;
@@ -374,7 +382,9 @@ __device__ __forceinline__ void kv_exec(const Params& P, Rep<NT>& x, uint32_t cm
 template <int NT>
 __device__ __forceinline__ void paxos_exec(const Params& P, Rep<NT>& x) {     // paxos.go:345-369
   for (;;) {
-    if (hbm_log(x) && x.execute > x.slot) break;                   // entries exist only up to p.slot (saves an HBM read)
+    if (hbm_log(x)) {                                              // skip the HBM read of an uncommitted entry
+      if (P.W <= 16u ? !((x.cmask >> ((uint32_t)x.execute & (P.W - 1u))) & 1u) : x.execute > x.slot) break;
+    }
     const uint32_t i = eidx<NT>(P, x, x.execute);
     const uint32_t c = eb(x, i);
     if ((c & (EF_EXISTS | EF_COMMIT)) != (EF_EXISTS | EF_COMMIT)) break;

@@ -33,6 +33,7 @@ struct Rep {
   uint32_t e0, es;                      // log entry i of slot s: e0 + (s & (W-1)) * es
   uint4 ce;                             // HBM-resident window (es = 4): entry at word ci, cached (paxos_kernel.h)
   uint32_t ci;
+  uint32_t cmask;                       // HBM-resident window: committed entries, one bit per window slot (W <= 16)
   uint32_t* reqx;                       // request side table, indexed like the log
   uint32_t* pend;                       // pending request k at pend[k * pstride]
   uint32_t pstride;
@@ -111,32 +112,68 @@ __device__ __forceinline__ bool send_begin(const Params& P, Rep<NT>& x, uint32_t
   return true;
 }
 
+// The scripted faults of this replica at this step (socket.go:163-199 Drop /
+// Slow / Flaky / Crash windows), in one pass over the table: a crash flag and,
+// per destination, drop / flaky bits and the largest Slow delay (4 bits each).
+// The table is uniform across the wave; its three loads per fault go out
+// together (one round trip per fault, not one per (kind, destination) query).
+struct ScriptedStep {
+  uint32_t drop, flaky;
+  uint64_t slow;
+  bool crash;
+};
+template <int NT>
+__device__ __forceinline__ ScriptedStep scripted_scan(const Params& P, const Rep<NT>& x) {
+  ScriptedStep o = {0u, 0u, 0ull, false};
+  const uint32_t N = nrep<NT>(P);
+  for (uint32_t i = 0; i < P.nfaults; i++) {
+    const uint32_t* fw = reinterpret_cast<const uint32_t*>(&P.faults[i]);
+    const uint4 a = *reinterpret_cast<const uint4*>(fw);          // kind, src, dst, param
+    const uint4 b = *reinterpret_cast<const uint4*>(fw + 4);      // cluster_lo, cluster_hi
+    const uint2 c = *reinterpret_cast<const uint2*>(fw + 8);      // step_from, step_to
+    if (a.y != x.r) continue;
+    const uint64_t lo = (uint64_t)b.x | ((uint64_t)b.y << 32), hi = (uint64_t)b.z | ((uint64_t)b.w << 32);
+    if (x.gid < lo || x.gid >= hi || x.t < c.x || x.t >= c.y) continue;
+    if (a.x == PAXISIM_FAULT_CRASH) {
+      o.crash = true;
+      continue;
+    }
+    const uint32_t dst = a.z == PAXISIM_ALL_DST ? ((1u << N) - 1u) : (a.z < N ? 1u << a.z : 0u);
+    if (a.x == PAXISIM_FAULT_DROP) o.drop |= dst;
+    if (a.x == PAXISIM_FAULT_FLAKY && a.w > 0) o.flaky |= dst;
+    if (a.x == PAXISIM_FAULT_SLOW) {
+#pragma unroll
+      for (uint32_t d = 0; d < Rep<NT>::NL; d++) {
+        const uint64_t cur = (o.slow >> (4u * d)) & 15u;
+        if (((dst >> d) & 1u) && a.w > cur) o.slow = (o.slow & ~(15ull << (4u * d))) | ((uint64_t)a.w << (4u * d));
+      }
+    }
+  }
+  return o;
+}
+
 // Per step: fold crash / drop / slow / flaky of every outgoing link into masks
 // (the filter order crash -> drop -> flaky -> slow is kept by send_begin).
 template <int NT>
 __device__ __forceinline__ void link_masks(const Params& P, Rep<NT>& x, const uint32_t (&du)[Rep<NT>::NL],
-                                           const uint32_t (&su)[Rep<NT>::NL]) {
+                                           const uint32_t (&su)[Rep<NT>::NL], const ScriptedStep& sc) {
   const uint32_t N = nrep<NT>(P);
-  uint32_t dm = 0, fm = 0;
+  uint32_t dm = 0;
   uint64_t dl = 0;
 #pragma unroll
   for (uint32_t d = 0; d < Rep<NT>::NL; d++) {
     if (d >= N) continue;
     uint32_t delay = 0;
-    bool drop = x.t < du[d];
+    const bool drop = x.t < du[d] || ((sc.drop >> d) & 1u);
     if (x.t < (su[d] & (T_MAX - 1u))) delay = su[d] >> 28;
-    if (P.nfaults) {
-      drop = drop || scripted(P, PAXISIM_FAULT_DROP, x.gid, x.r, d, x.t, nullptr);
-      uint32_t p = 0;
-      if (scripted(P, PAXISIM_FAULT_FLAKY, x.gid, x.r, d, x.t, &p) && p > 0) fm |= 1u << d;
-      scripted(P, PAXISIM_FAULT_SLOW, x.gid, x.r, d, x.t, &delay);
-    }
+    const uint32_t sd = (uint32_t)(sc.slow >> (4u * d)) & 15u;
+    if (sd > delay) delay = sd;
     if (delay > P.max_delay) delay = P.max_delay;
     dm |= (drop || x.crashed) ? (1u << d) : 0u;
     dl |= (uint64_t)delay << (4u * d);
   }
   x.dmask = dm;
-  x.fmask = fm;
+  x.fmask = sc.flaky;
   x.dly = dl;
 }
 
@@ -267,26 +304,29 @@ __device__ __forceinline__ uint32_t wl_hash(uint32_t kc, uint32_t cid) { return 
 // With locality (WPaxos per-zone clients, benchmark.go:202-213 "conflict"/Min):
 // worker w's command is, with P = locality, one of the keys k = z (mod Z) of
 // the zone z of its target replica, otherwise uniform over all keys.
+// x % d for d >= 1 given m = floor((2^32-1)/d): the quotient estimate is low by at most one
+__device__ __forceinline__ uint32_t mod_magic(uint32_t x, uint32_t d, uint32_t m) {
+  uint32_t r = x - d * __umulhi(x, m);
+  return r >= d ? r - d : r;
+}
 __device__ __forceinline__ uint32_t wl_key(const Params& P, uint32_t kc, uint32_t cid) {
   const uint32_t h = wl_hash(kc, cid);
   if (P.locality_ppm) {
-    uint32_t w = (cid - 1u) - P.WK * __umulhi(cid - 1u, P.wk_magic);   // (cid-1) % WK
-    if (w >= P.WK) w -= P.WK;
-    const uint32_t z = P.zone_of[P.target[w]];
-    const uint32_t nk = z < P.keys ? (P.keys - z + P.Z - 1u) / P.Z : 0u;
-    if (nk && ppm_hit(fmix32(h ^ 0x165667B1u), P.locality_ppm)) return z + P.Z * (h % nk);
+    const uint32_t w = mod_magic(cid - 1u, P.WK, P.wk_magic);        // (cid-1) % WK
+    const uint32_t z = P.wzone[w], nk = P.wnk[w];                    // zone_of[target[w]], its key count
+    if (nk && ppm_hit(fmix32(h ^ 0x165667B1u), P.locality_ppm)) return z + P.Z * mod_magic(h, nk, P.wnk_magic[w]);
   }
   switch (P.dist) {   // Bconfig.Distribution (benchmark.go:202-233), DESIGN.md §3.8
-    case PAXISIM_DIST_ORDER: return cid % P.keys;
+    case PAXISIM_DIST_ORDER: return mod_magic(cid, P.keys, P.keys_magic);
     case PAXISIM_DIST_CONFLICT:
-      return fmix32(h ^ 0x3C6EF372u) % 100u < P.conflicts ? 0u : cid % P.keys;
+      return fmix32(h ^ 0x3C6EF372u) % 100u < P.conflicts ? 0u : mod_magic(cid, P.keys, P.keys_magic);
     case PAXISIM_DIST_TABLE: {   // inverse CDF; the table index is uniform, so these are scalar loads
       const uint32_t u = fmix32(h ^ 0x2545F491u);
       uint32_t k = 0;
       for (uint32_t i = 0; i + 1u < P.keys; i++) k += u >= P.key_cdf[i] ? 1u : 0u;
       return k;
     }
-    default: return h % P.keys;
+    default: return mod_magic(h, P.keys, P.keys_magic);
   }
 }
 __device__ __forceinline__ bool wl_write(const Params& P, uint32_t kc, uint32_t cid) {
@@ -458,15 +498,18 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
   x.hs = step_key(x.kc, x.t);
   if (P.late_workers) client_start<NT>(P, x);
   {
+    // link state exists only under a random fault process (without one it stays 0)
+    const bool random_faults = P.drop_ppm || P.slow_ppm;
     uint32_t du[Rep<NT>::NL], su[Rep<NT>::NL];
 #pragma unroll
     for (uint32_t d = 0; d < Rep<NT>::NL; d++) {
-      du[d] = d < N ? P.link_drop[krc(P, d, x.r, x.c)] : 0u;
-      su[d] = d < N ? P.link_slow[krc(P, d, x.r, x.c)] : 0u;
+      du[d] = d < N && random_faults ? P.link_drop[krc(P, d, x.r, x.c)] : 0u;
+      su[d] = d < N && random_faults ? P.link_slow[krc(P, d, x.r, x.c)] : 0u;
     }
     fault_process<NT>(P, x, du, su);
-    x.crashed = P.nfaults && scripted(P, PAXISIM_FAULT_CRASH, x.gid, x.r, 0u, x.t, nullptr);
-    link_masks<NT>(P, x, du, su);
+    const ScriptedStep sc = P.nfaults ? scripted_scan<NT>(P, x) : ScriptedStep{0u, 0u, 0ull, false};
+    x.crashed = sc.crash;
+    link_masks<NT>(P, x, du, su, sc);
   }
 
   const uint32_t box0 = (x.b0 * N + x.r) * NS;          // inbox boxes: box0 + src

@@ -17,7 +17,7 @@
 // replica, lane) so that one lane's state, window and pending list are each
 // contiguous:
 //   wst   [blk][K][N][64] x 32 B  {ballot, slot, execute, active|exists<<1|wovf,ghost<<2|p1acks<<16,
-//                                   npend, digest, policy last|hits<<8}
+//                                   npend, digest, policy last|hits<<8 | committed window slots<<16}
 //   wlog  [blk][K][N][64][W] x 16 B {ballot, cmd|flags, acks, request}
 //   wpend [blk][K][N][64][PMAX] x 4 B
 #pragma once
@@ -55,7 +55,8 @@ __device__ __forceinline__ void wp_bind(const Params& P, Rep<NT>& x, uint32_t ke
   x.p1mask = a.w >> 16;
   x.npend = b.x;
   x.digest = (uint64_t)b.y | ((uint64_t)b.z << 32);
-  x.pol = b.w;
+  x.pol = b.w & 0xFFFFu;
+  x.cmask = b.w >> 16;
   uint32_t* lb = P.wlog + si * P.W * 4u;
   x.l_a = lb;
   x.l_b = lb + 1;
@@ -69,7 +70,7 @@ __device__ __forceinline__ void wp_unbind(const Params& P, const Rep<NT>& x) {
   const size_t si = wp_slot<NT>(P, x, x.key);
   P.wst[2 * si] = make_uint4(x.ballot, (uint32_t)x.slot, (uint32_t)x.execute,
                              (x.active & 1u) | (x.exists << 1) | (x.iflags << 2) | (x.p1mask << 16));
-  P.wst[2 * si + 1] = make_uint4(x.npend, (uint32_t)x.digest, (uint32_t)(x.digest >> 32), x.pol);
+  P.wst[2 * si + 1] = make_uint4(x.npend, (uint32_t)x.digest, (uint32_t)(x.digest >> 32), x.pol | (x.cmask << 16));
 }
 
 // r.paxi[m.Key] without a prior init: a nil *kpaxos, whose use panics in Go
