@@ -595,6 +595,35 @@ __device__ __forceinline__ void paxos_handle_p3(const Params& P, Rep<NT>& x, uin
   if (!P.rwc) paxos_exec<NT>(P, x);
 }
 
+// HandleP2b (paxos.go:270-310) for a P2b that neither completes a quorum nor
+// poisons, on the bound instance: returns true after applying it exactly as
+// paxos_handle_p2b would (ignored: no entry (G7), m.Ballot < e.ballot,
+// committed, or outside the window where no flag can be raised; else adopt a
+// higher ballot and record the ack).  Returns false, with no effect, for every
+// other P2b.
+template <int NT>
+__device__ __forceinline__ bool p2b_absorb(const Params& P, Rep<NT>& x, uint32_t src, const uint4& m) {
+  const int32_t ms = (int32_t)m.z;
+  const uint32_t mb = m.y;
+  if (!in_window<NT>(P, x, ms))
+    return ms < x.execute ? !(x.iflags & PAXISIM_F_GHOST) : !(x.iflags & PAXISIM_F_WOVF);
+  const uint32_t i = eidx<NT>(P, x, ms);
+  const uint32_t c = eb(x, i);
+  const uint32_t eb0 = ea(x, i);
+  if (!(c & EF_EXISTS) || mb < eb0 || (c & EF_COMMIT)) return true;
+  if (bal_id(mb) == x.r && mb == eb0) {
+    if (!(c & EF_QUORUM)) return false;                 // nil quorum: the full handler poisons
+    const uint32_t ack = ec(x, i) | (1u << src);
+    if (quorum_ok(P, P.q2, ack)) return false;          // commit: the full handler
+    set_c(x, i, ack);
+  }
+  if (mb > x.ballot) {
+    x.ballot = mb;
+    x.active = 0;
+  }
+  return true;
+}
+
 // ---------------------------------------------------------------------------
 // protocol policy
 // ---------------------------------------------------------------------------
@@ -638,33 +667,10 @@ struct PaxosProto {
   __device__ static __forceinline__ void client_request(const Params& P, Rep<NT>& x, uint32_t cid) {
     handle_request<NT>(P, x, mkreq(cid, PAXISIM_CLIENT_SRC));
   }
-  // HandleP2b (paxos.go:270-310) for a P2b that neither completes a quorum
-  // nor poisons: returns true after applying it exactly as paxos_handle_p2b
-  // would (ignored: no entry (G7), m.Ballot < e.ballot, committed, or outside
-  // the window where no flag can be raised; else adopt a higher ballot and
-  // record the ack).  Returns false, with no effect, for every other message.
+  // a P2b that completes no quorum is handled in the trip before it (sim_core.h)
   template <int NT>
   __device__ static __forceinline__ bool absorb(const Params& P, Rep<NT>& x, uint32_t src, const uint4& m) {
-    if (hdr_type(m.x) != PAXISIM_MSG_P2B) return false;
-    const int32_t ms = (int32_t)m.z;
-    const uint32_t mb = m.y;
-    if (!in_window<NT>(P, x, ms))
-      return ms < x.execute ? !(x.iflags & PAXISIM_F_GHOST) : !(x.iflags & PAXISIM_F_WOVF);
-    const uint32_t i = eidx<NT>(P, x, ms);
-    const uint32_t c = eb(x, i);
-    const uint32_t eb0 = ea(x, i);
-    if (!(c & EF_EXISTS) || mb < eb0 || (c & EF_COMMIT)) return true;
-    if (bal_id(mb) == x.r && mb == eb0) {
-      if (!(c & EF_QUORUM)) return false;                 // nil quorum: the full handler poisons
-      const uint32_t ack = ec(x, i) | (1u << src);
-      if (quorum_ok(P, P.q2, ack)) return false;          // commit: the full handler
-      set_c(x, i, ack);
-    }
-    if (mb > x.ballot) {
-      x.ballot = mb;
-      x.active = 0;
-    }
-    return true;
+    return hdr_type(m.x) == PAXISIM_MSG_P2B && p2b_absorb<NT>(P, x, src, m);
   }
   // node.handle dispatch (node.go:104-115; registrations paxos/replica.go:33-38)
   template <int NT>

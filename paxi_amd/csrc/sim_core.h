@@ -203,7 +203,7 @@ __device__ __forceinline__ void broadcast1(const Params& P, Rep<NT>& x, uint32_t
 // records in exactly the order the handlers issued them.
 // ---------------------------------------------------------------------------
 #ifndef PXS_FLUSH1_9
-#define PXS_FLUSH1_9 1   // 9-replica WPaxos kernel: one pass per destination (no 2 x 9 transient registers)
+#define PXS_FLUSH1_9 0   // 1: 9-replica WPaxos kernel flushes in one pass (A/B r2: +4% at 153 spilled VGPRs, -3% at 101)
 #endif
 template <int NT>
 __device__ __forceinline__ void intent_flush(const Params& P, Rep<NT>& x) {
