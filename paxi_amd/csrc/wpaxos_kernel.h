@@ -256,6 +256,7 @@ struct WPaxosProto {
       ecache<NT>(x, (m.z & (P.W - 1u)) * 4u);
       PXS_CASE_T1(14)
     }
+    bool clean = false;                                                // instance state unchanged
     switch (type) {
       case PAXISIM_MSG_REQUEST:
         { PXS_CASE_T0
@@ -286,7 +287,11 @@ struct WPaxosProto {
       case PAXISIM_MSG_P2B:                                            // handleAccepted 90-93
         { PXS_CASE_T0
         dv_inc<NT>(x, PAXISIM_MSG_P2B);
+        // most P2bs change only their entry (an ack, or nothing): the instance
+        // state then needs no write-back
+        const uint32_t b0 = x.ballot, e0 = (uint32_t)x.execute, f0 = x.iflags, m0 = x.cmask;
         if (wp_get<NT>(x)) paxos_handle_p2b<NT>(P, x, src, m.y, (int32_t)m.z);
+        clean = !x.stop && x.ballot == b0 && (uint32_t)x.execute == e0 && x.iflags == f0 && x.cmask == m0;
         PXS_CASE_T1(PAXISIM_MSG_P2B) }
         break;
       case PAXISIM_MSG_P3:                                             // handleCommit 95-99
@@ -306,7 +311,7 @@ struct WPaxosProto {
     }
     {
       PXS_CASE_T0
-      wp_unbind<NT>(P, x);
+      if (!clean) wp_unbind<NT>(P, x);
       PXS_CASE_T1(15)
     }
   }
