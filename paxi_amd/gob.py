@@ -89,13 +89,22 @@ ABD_GET = Struct("Get", [("ID", ID), ("CID", INT), ("Key", KEY)])
 ABD_GETREPLY = Struct("GetReply", [("ID", ID), ("CID", INT), ("Key", KEY), ("Value", VALUE), ("Version", INT)])
 ABD_SET = Struct("Set", [("ID", ID), ("CID", INT), ("Key", KEY), ("Value", VALUE), ("Version", INT)])
 ABD_SETREPLY = Struct("SetReply", [("ID", ID), ("CID", INT), ("Key", KEY)])
-# wpaxos/msg.go:22-84: the embedded paxos message is a field named after its type
-WP_PREPARE = Struct("Prepare", [("Key", KEY), ("P1a", P1A)])
-WP_PROMISE = Struct("Promise", [("Key", KEY), ("P1b", P1B)])
-WP_ACCEPT = Struct("Accept", [("Key", KEY), ("P2a", P2A)])
-WP_ACCEPTED = Struct("Accepted", [("Key", KEY), ("P2b", P2B)])
-WP_COMMIT = Struct("Commit", [("Key", KEY), ("P3", P3)])
-WP_LEADERCHANGE = Struct("LeaderChange", [("Key", KEY), ("To", ID), ("From", ID), ("Ballot", BALLOT)])
+# wpaxos/msg.go:22-84, m2paxos/msg.go:25-80, kpaxos/msg.go:25-80: one set of
+# per-key wrappers per package (distinct Go types of the same shape); the
+# embedded paxos message is a field named after its type
+def _keyed():
+    return {"Prepare": Struct("Prepare", [("Key", KEY), ("P1a", P1A)]),
+            "Promise": Struct("Promise", [("Key", KEY), ("P1b", P1B)]),
+            "Accept": Struct("Accept", [("Key", KEY), ("P2a", P2A)]),
+            "Accepted": Struct("Accepted", [("Key", KEY), ("P2b", P2B)]),
+            "Commit": Struct("Commit", [("Key", KEY), ("P3", P3)]),
+            "LeaderChange": Struct("LeaderChange", [("Key", KEY), ("To", ID), ("From", ID), ("Ballot", BALLOT)])}
+
+
+KEYED = {pkg: _keyed() for pkg in ("wpaxos", "m2paxos", "kpaxos")}
+WP_PREPARE, WP_PROMISE, WP_ACCEPT = KEYED["wpaxos"]["Prepare"], KEYED["wpaxos"]["Promise"], KEYED["wpaxos"]["Accept"]
+WP_ACCEPTED, WP_COMMIT = KEYED["wpaxos"]["Accepted"], KEYED["wpaxos"]["Commit"]
+WP_LEADERCHANGE = KEYED["wpaxos"]["LeaderChange"]
 
 # gob.Register names: the package path "." the type name (the reference builds
 # under the GOPATH import path github.com/ailidani/paxi)
@@ -106,10 +115,8 @@ REGISTERED = {
     f"{PKG}/paxos.P3": P3,
     f"{PKG}/abd.Get": ABD_GET, f"{PKG}/abd.GetReply": ABD_GETREPLY, f"{PKG}/abd.Set": ABD_SET,
     f"{PKG}/abd.SetReply": ABD_SETREPLY,
-    f"{PKG}/wpaxos.Prepare": WP_PREPARE, f"{PKG}/wpaxos.Promise": WP_PROMISE, f"{PKG}/wpaxos.Accept": WP_ACCEPT,
-    f"{PKG}/wpaxos.Accepted": WP_ACCEPTED, f"{PKG}/wpaxos.Commit": WP_COMMIT,
-    f"{PKG}/wpaxos.LeaderChange": WP_LEADERCHANGE,
 }
+REGISTERED.update({f"{PKG}/{pkg}.{name}": t for pkg, types in KEYED.items() for name, t in types.items()})
 
 
 # ---- primitives -------------------------------------------------------------

@@ -30,6 +30,7 @@ Messages map to Paxi values as follows (a ballot is the 64-bit
            Set{...} / SetReply{ID, CID, Key}                   (abd/msg.go:16-46)
   WPaxos   wpaxos.Prepare{Key, P1a} / Promise{Key, P1b} / Accept{Key, P2a} /
            Accepted{Key, P2b} / Commit{Key, P3} / LeaderChange{Key, To, From, Ballot}
+           (M2Paxos and KPaxos: the same shapes in packages m2paxos and kpaxos)
 A Command is {Key = Bconfig.Min + key, Value = Uvarint(cid) in a 10-byte buffer
 for a write (client/client.go:42-45) or nil for a read, ClientID "", CommandID
 = cid}; the simulator derives key and kind from the command id
@@ -50,11 +51,15 @@ T_GET, T_GETREPLY, T_SET, T_SETREPLY, T_LEADERCHG = 9, 10, 11, 12, 13
 P = gob.PKG
 PAXOS_NAMES = {T_P1A: f"{P}/paxos.P1a", T_P1B: f"{P}/paxos.P1b", T_P2A: f"{P}/paxos.P2a",
                T_P2B: f"{P}/paxos.P2b", T_P3: f"{P}/paxos.P3"}
-WPAXOS_NAMES = {T_P1A: f"{P}/wpaxos.Prepare", T_P1B: f"{P}/wpaxos.Promise", T_P2A: f"{P}/wpaxos.Accept",
-                T_P2B: f"{P}/wpaxos.Accepted", T_P3: f"{P}/wpaxos.Commit", T_LEADERCHG: f"{P}/wpaxos.LeaderChange"}
+_KEYED = {T_P1A: "Prepare", T_P1B: "Promise", T_P2A: "Accept", T_P2B: "Accepted", T_P3: "Commit",
+          T_LEADERCHG: "LeaderChange"}
+# the per-key protocols' wrappers, one package each (wpaxos/, m2paxos/, kpaxos/ msg.go)
+KEYED_NAMES = {proto: {t: f"{P}/{pkg}.{n}" for t, n in _KEYED.items()}
+               for proto, pkg in ((abi.WPAXOS, "wpaxos"), (abi.M2PAXOS, "m2paxos"), (abi.KPAXOS, "kpaxos"))}
+WPAXOS_NAMES = KEYED_NAMES[abi.WPAXOS]
 ABD_NAMES = {T_GET: f"{P}/abd.Get", T_GETREPLY: f"{P}/abd.GetReply", T_SET: f"{P}/abd.Set",
              T_SETREPLY: f"{P}/abd.SetReply"}
-NAME_TYPE = {v: k for d in (PAXOS_NAMES, WPAXOS_NAMES, ABD_NAMES) for k, v in d.items()}
+NAME_TYPE = {v: k for d in (PAXOS_NAMES, ABD_NAMES, *KEYED_NAMES.values()) for k, v in d.items()}
 NAME_TYPE[f"{P}.Request"] = T_REQUEST
 NAME_TYPE[f"{P}.Reply"] = T_REPLY
 
@@ -179,14 +184,14 @@ class Codec:
             v = {"Ballot": top.ballot64(b), "Slot": s, "Command": self.command(cid)}
         elif t == T_P2B:
             v = {"Ballot": top.ballot64(b), "ID": top.id(src), "Slot": s}
-        elif t == T_LEADERCHG and self.proto == abi.WPAXOS:
-            return WPAXOS_NAMES[t], {"Key": self.key_min + key, "To": top.id(s), "From": top.id(cid),
-                                     "Ballot": top.ballot64(b)}
+        elif t == T_LEADERCHG and self.proto in abi.PER_KEY:
+            return KEYED_NAMES[self.proto][t], {"Key": self.key_min + key, "To": top.id(s), "From": top.id(cid),
+                                                "Ballot": top.ballot64(b)}
         else:
             raise TraceError(f"message type {t} has no Paxi wire form here")
-        if self.proto == abi.WPAXOS:
+        if self.proto in abi.PER_KEY:
             inner = {T_P1A: "P1a", T_P1B: "P1b", T_P2A: "P2a", T_P2B: "P2b", T_P3: "P3"}[t]
-            return WPAXOS_NAMES[t], {"Key": self.key_min + key, inner: v}
+            return KEYED_NAMES[self.proto][t], {"Key": self.key_min + key, inner: v}
         return PAXOS_NAMES[t], v
 
     # (name, value) -> records
@@ -205,7 +210,9 @@ class Codec:
             return [(src, t | (k << 8), v["CID"], v.get("Version", 0) if t in (T_GETREPLY, T_SET) else 0,
                      read_uvarint(val) if val else 0)]
         key = 0
-        if self.proto == abi.WPAXOS:
+        if self.proto in abi.PER_KEY:
+            if name not in KEYED_NAMES[self.proto].values():
+                raise TraceError(f"{name} is not a message of this protocol")
             key = v["Key"] - self.key_min
             if t == T_LEADERCHG:
                 return [(src, t | (key << 16), top.ballot32(v["Ballot"]), top.replica(v["To"]),

@@ -144,7 +144,18 @@ def abd_case(clusters=4, base=0):
     return cfg, wl, None
 
 
-CASES = {"paxos": paxos_case, "wpaxos": wpaxos_case, "abd": abd_case}
+def perkey_case(proto):
+    def mk(clusters=4, base=0):
+        cfg = abi.make_config(protocol=proto, npz=[3, 3, 3], keys=16, clusters=clusters, cluster_base=base,
+                              seed=9, window=16, mbox_cap=24, max_delay=0)
+        wl = abi.make_workload(outstanding=9, target=list(range(9)), locality_ppm=700_000, key_min=192,
+                               write_ppm=500_000)
+        return cfg, wl, None
+    return mk
+
+
+CASES = {"paxos": paxos_case, "wpaxos": wpaxos_case, "abd": abd_case, "m2paxos": perkey_case(abi.M2PAXOS),
+         "kpaxos": perkey_case(abi.KPAXOS)}
 KEEP = lambda t: t[:11] + t[12:14] + t[15:]   # replica state minus dropped and replies (the replay drops every send)
 
 
@@ -168,7 +179,7 @@ def replay_from_zero(backend, case, cluster=3, steps=150, tmpdir=None):
     return a, b, tr, streams, sa, sb
 
 
-@pytest.mark.parametrize("case", ["paxos", "wpaxos", "abd"])
+@pytest.mark.parametrize("case", ["paxos", "wpaxos", "abd", "m2paxos", "kpaxos"])
 def test_replay_oracle(case, tmp_path):
     a, b, tr, streams, sa, sb = replay_from_zero(OracleSim, case, tmpdir=str(tmp_path))
     assert len(tr["msgs"]) > 100 and len(streams) >= 4
@@ -190,6 +201,20 @@ def test_trace_stream_per_link_is_fifo():
         want = [codec.to_go(s, recs) for (t, s, d, recs) in tr["msgs"] if (s, d) == (src, dst)]
         assert list(gob.Decoder(data)) == [(n, gob.full(gob.REGISTERED[n], v)) for n, v in want]
         assert sched["links"][f"{src}->{dst}"] == sorted(sched["links"][f"{src}->{dst}"])
+
+
+def test_keyed_protocols_use_their_own_package():
+    """m2paxos.Accept and wpaxos.Accept are distinct registered Go types: each
+    protocol exports its own, and imports refuse the other's."""
+    cfg, wl, _ = CASES["m2paxos"]()
+    a = OracleSim(cfg, wl)
+    tr = trace.capture(a, 1, 40)
+    streams, sched = trace.export(a, 1, tr)
+    names = {n for data in streams.values() for n, _ in gob.Decoder(data)}
+    assert names and all(n.startswith(f"{P}/m2paxos.") or n in (f"{P}.Request", f"{P}.Reply") for n in names)
+    codec = trace.Codec(a, 1)
+    with pytest.raises(trace.TraceError):
+        codec.from_go(0, f"{P}/wpaxos.Prepare", {"Key": 192, "P1a": {"Ballot": 4295032833}})
 
 
 def test_import_rejects_foreign_commands():
@@ -220,7 +245,7 @@ def test_read_inbox_parity_gpu(case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["paxos", "wpaxos", "abd"])
+@pytest.mark.parametrize("case", ["paxos", "wpaxos", "abd", "m2paxos", "kpaxos"])
 def test_replay_gpu(case):
     """Capture on the GPU, gob export and import, replay on the GPU: the replayed
     cluster retraces the captured one, and both equal the oracle's."""
