@@ -187,8 +187,8 @@ def cpu_baseline(args, min_s=3.0):
     threads, why = cpu_threads()
     warm, window = args.warmup * args.sim_steps, args.steps * args.sim_steps
     out = {}
-    clusters = 256
-    for nthr in (1, threads):
+
+    def sample(nthr, clusters):
         cfg, wl, fp, faults, _ = workload(args.config, clusters, 0, 0, args)
         o = oracle_lib.OracleSim(cfg, wl, fp, faults)
         o.step(warm, threads=nthr)
@@ -197,13 +197,16 @@ def cpu_baseline(args, min_s=3.0):
         o.step(window, threads=nthr)
         dt = time.perf_counter() - t0
         s1 = o.stats().as_dict()
-        out[nthr] = ((s1["delivered_total"] - s0["delivered_total"]) / dt, (s1["commits"] - s0["commits"]) / dt,
-                     dt, clusters)
         o.close()
-        if nthr == 1:   # size the multi-thread sample for >= min_s seconds
-            clusters = int(256 * threads * max(1.0, min_s / max(dt, 1e-3)))
-        if threads == 1:
-            break
+        return ((s1["delivered_total"] - s0["delivered_total"]) / dt, (s1["commits"] - s0["commits"]) / dt,
+                dt, clusters)
+
+    out[1] = sample(1, 256)
+    if out[1][2] < 2.0:   # a single-thread sample of >= 2 s
+        out[1] = sample(1, int(256 * 2.2 / max(out[1][2], 1e-3)))
+    if threads > 1:       # the multi-thread sample sized for >= min_s seconds
+        dt1, cl1 = out[1][2], out[1][3]
+        out[threads] = sample(threads, int(cl1 * threads * max(1.0, min_s / max(dt1, 1e-3))))
     v, c, dt, cl = out[threads]
     v1, _, dt1, cl1 = out[1]
     cpu = "unknown"
