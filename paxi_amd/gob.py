@@ -102,6 +102,16 @@ def _keyed():
 
 
 KEYED = {pkg: _keyed() for pkg in ("wpaxos", "m2paxos", "kpaxos")}
+# epaxos/msg.go:18-65: instance messages with dependency maps
+DEPS = Map("map[paxi.ID]int", ID, INT)
+EP_PREACCEPT = Struct("PreAccept", [("Ballot", BALLOT), ("Replica", ID), ("Slot", INT), ("Command", COMMAND),
+                                    ("Seq", INT), ("Dep", DEPS)])
+EP_PREACCEPTREPLY = Struct("PreAcceptReply", [("Ballot", BALLOT), ("Replica", ID), ("Slot", INT), ("Seq", INT),
+                                              ("Dep", DEPS), ("Committed", DEPS)])
+EP_ACCEPT = Struct("Accept", [("Ballot", BALLOT), ("Replica", ID), ("Slot", INT), ("Seq", INT), ("Dep", DEPS)])
+EP_ACCEPTREPLY = Struct("AcceptReply", [("Ballot", BALLOT), ("Replica", ID), ("Slot", INT)])
+EP_COMMIT = Struct("Commit", [("Ballot", BALLOT), ("Replica", ID), ("Slot", INT), ("Command", COMMAND),
+                              ("Seq", INT), ("Dep", DEPS)])
 WP_PREPARE, WP_PROMISE, WP_ACCEPT = KEYED["wpaxos"]["Prepare"], KEYED["wpaxos"]["Promise"], KEYED["wpaxos"]["Accept"]
 WP_ACCEPTED, WP_COMMIT = KEYED["wpaxos"]["Accepted"], KEYED["wpaxos"]["Commit"]
 WP_LEADERCHANGE = KEYED["wpaxos"]["LeaderChange"]
@@ -117,6 +127,9 @@ REGISTERED = {
     f"{PKG}/abd.SetReply": ABD_SETREPLY,
 }
 REGISTERED.update({f"{PKG}/{pkg}.{name}": t for pkg, types in KEYED.items() for name, t in types.items()})
+REGISTERED.update({f"{PKG}/epaxos.PreAccept": EP_PREACCEPT, f"{PKG}/epaxos.PreAcceptReply": EP_PREACCEPTREPLY,
+                   f"{PKG}/epaxos.Accept": EP_ACCEPT, f"{PKG}/epaxos.AcceptReply": EP_ACCEPTREPLY,
+                   f"{PKG}/epaxos.Commit": EP_COMMIT})
 
 
 # ---- primitives -------------------------------------------------------------

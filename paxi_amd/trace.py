@@ -36,7 +36,8 @@ for a write (client/client.go:42-45) or nil for a read, ClientID "", CommandID
 = cid}; the simulator derives key and kind from the command id
 (paxisim_commands), so an imported command must agree with them.  Not carried
 (the simulator has no such state): a Request's Timestamp and Properties, a
-Reply's Value / Properties / Err.  EPaxos traces are not exported.
+Reply's Value / Properties / Err.
+  EPaxos   epaxos.PreAccept / PreAcceptReply / Accept / AcceptReply / Commit (epaxos/msg.go:18-65)
 """
 from __future__ import annotations
 
@@ -47,6 +48,7 @@ from . import abi, gob
 
 T_REQUEST, T_REPLY, T_P1A, T_P1B, T_P1B_ENTRY, T_P2A, T_P2B, T_P3 = 1, 2, 3, 4, 5, 6, 7, 8
 T_GET, T_GETREPLY, T_SET, T_SETREPLY, T_LEADERCHG = 9, 10, 11, 12, 13
+T_PREACCEPT, T_PREACCEPTREPLY, T_ACCEPT, T_ACCEPTREPLY, T_COMMIT = 14, 15, 16, 17, 18
 
 P = gob.PKG
 PAXOS_NAMES = {T_P1A: f"{P}/paxos.P1a", T_P1B: f"{P}/paxos.P1b", T_P2A: f"{P}/paxos.P2a",
@@ -59,7 +61,9 @@ KEYED_NAMES = {proto: {t: f"{P}/{pkg}.{n}" for t, n in _KEYED.items()}
 WPAXOS_NAMES = KEYED_NAMES[abi.WPAXOS]
 ABD_NAMES = {T_GET: f"{P}/abd.Get", T_GETREPLY: f"{P}/abd.GetReply", T_SET: f"{P}/abd.Set",
              T_SETREPLY: f"{P}/abd.SetReply"}
-NAME_TYPE = {v: k for d in (PAXOS_NAMES, ABD_NAMES, *KEYED_NAMES.values()) for k, v in d.items()}
+EPAXOS_NAMES = {T_PREACCEPT: f"{P}/epaxos.PreAccept", T_PREACCEPTREPLY: f"{P}/epaxos.PreAcceptReply",
+                T_ACCEPT: f"{P}/epaxos.Accept", T_ACCEPTREPLY: f"{P}/epaxos.AcceptReply", T_COMMIT: f"{P}/epaxos.Commit"}
+NAME_TYPE = {v: k for d in (PAXOS_NAMES, ABD_NAMES, EPAXOS_NAMES, *KEYED_NAMES.values()) for k, v in d.items()}
 NAME_TYPE[f"{P}.Request"] = T_REQUEST
 NAME_TYPE[f"{P}.Reply"] = T_REPLY
 
@@ -93,6 +97,20 @@ class Topology:
             return 0
         z, n = self.ids[b & 15]
         return ((b >> 4) << 32) | (z << 16) | n
+
+    def ep_ballot64(self, b):
+        """EPaxos ballots are NewBallot(0, owner) (epaxos/replica.go:114), kept as 1 + owner index."""
+        if b == 0:
+            return 0
+        z, n = self.ids[b - 1]
+        return (z << 16) | n
+
+    def ep_ballot32(self, b):
+        if b == 0:
+            return 0
+        if b >> 32:
+            raise TraceError("EPaxos ballots carry n = 0 here")
+        return 1 + self.replica(f"{(b >> 16) & 0xFFFF}.{b & 0xFFFF}")
 
     def ballot32(self, b):
         if b == 0:
@@ -158,14 +176,19 @@ class Codec:
 
     # records (one message: a header record and its payload records) -> (name, value)
     def to_go(self, src, recs):
-        self._commands([r[4] for r in recs])
         hdr, b, s, cid = recs[0][1:]
+        if self.proto != abi.EPAXOS:
+            self._commands([r[4] for r in recs])
+        elif (hdr & 0xFF) in (T_PREACCEPT, T_COMMIT):
+            self._commands([cid])
         t, key = hdr & 0xFF, hdr >> 16
         top = self.top
         if t == T_REQUEST:
             return f"{P}.Request", {"Command": self.command(cid), "NodeID": top.id(src)}
         if t == T_REPLY:
             return f"{P}.Reply", {"Command": self.command(cid)}
+        if self.proto == abi.EPAXOS:
+            return self._ep_to_go(src, t, b, s, cid, [w for r in recs[1:] for w in r[1:]])
         if self.proto == abi.ABD:
             k = self.key_min + ((hdr >> 8) & 0xFF)
             v = {"ID": top.id(src), "CID": b, "Key": k}
@@ -194,6 +217,47 @@ class Codec:
             return KEYED_NAMES[self.proto][t], {"Key": self.key_min + key, inner: v}
         return PAXOS_NAMES[t], v
 
+    # EPaxos (epaxos/msg.go:18-65): header {type | n << 8, ballot, slot, w3} + payload words
+    # PreAccept w3 = cmd, [seq, Dep[N]]; PreAcceptReply w3 = seq, [Dep[N], Committed[N]];
+    # Accept w3 = seq, [Dep[N]]; AcceptReply; Commit w3 = cmd, [seq, Dep[N]].  A Dep map holds
+    # the positive entries only (attributes / merge add an id only above the zero default,
+    # epaxos/replica.go:60-70, instance.go:29-40); Committed holds every id (-1 = none, replica.go:44).
+    def _ep_to_go(self, src, t, b, s, w3, pay):
+        top, N = self.top, self.top.N
+        i32 = lambda u: u - (1 << 32) if u >= 1 << 31 else u
+        deps = lambda ws: {top.id(k): i32(ws[k]) for k in range(N) if i32(ws[k]) > 0}
+        v = {"Ballot": top.ep_ballot64(b), "Replica": top.id(src), "Slot": s}
+        if t in (T_PREACCEPT, T_COMMIT):
+            v.update({"Command": self.command(w3), "Seq": i32(pay[0]), "Dep": deps(pay[1:1 + N])})
+        elif t == T_PREACCEPTREPLY:
+            v.update({"Seq": i32(w3), "Dep": deps(pay[:N]),
+                      "Committed": {top.id(k): i32(pay[N + k]) for k in range(N)}})
+        elif t == T_ACCEPT:
+            v.update({"Seq": i32(w3), "Dep": deps(pay[:N])})
+        elif t != T_ACCEPTREPLY:
+            raise TraceError(f"message type {t} has no EPaxos wire form")
+        return EPAXOS_NAMES[t], v
+
+    def _ep_from_go(self, src, t, v):
+        top, N = self.top, self.top.N
+        u32 = lambda x: x & 0xFFFFFFFF
+        dep = lambda m: [u32((m or {}).get(top.id(k), 0)) for k in range(N)]
+        b, s = top.ep_ballot32(v["Ballot"]), v["Slot"]
+        if t in (T_PREACCEPT, T_COMMIT):
+            w3, pay = self.check_command(v["Command"]), [u32(v["Seq"])] + dep(v["Dep"])
+        elif t == T_PREACCEPTREPLY:
+            com = v.get("Committed") or {}
+            if len(com) != N:
+                raise TraceError("PreAcceptReply.Committed must name every replica")
+            w3, pay = u32(v["Seq"]), dep(v["Dep"]) + [u32(com[top.id(k)]) for k in range(N)]
+        elif t == T_ACCEPT:
+            w3, pay = u32(v["Seq"]), dep(v["Dep"])
+        else:
+            w3, pay = 0, []
+        n = (len(pay) + 3) // 4
+        pay = pay + [0] * (4 * n - len(pay))
+        return [(src, t | (n << 8), b, s, w3)] + [(src, *pay[4 * k:4 * k + 4]) for k in range(n)]
+
     # (name, value) -> records
     def from_go(self, src, name, v):
         t = NAME_TYPE.get(name)
@@ -204,6 +268,10 @@ class Codec:
             return [(src, T_REQUEST, 0, 0, self.check_command(v["Command"]))]
         if t == T_REPLY:
             return [(src, T_REPLY, 0, 0, self.check_command(v["Command"]))]
+        if self.proto == abi.EPAXOS:
+            if name not in EPAXOS_NAMES.values():
+                raise TraceError(f"{name} is not an EPaxos message")
+            return self._ep_from_go(src, t, v)
         if t in (T_GET, T_GETREPLY, T_SET, T_SETREPLY):
             k = v["Key"] - self.key_min
             val = v.get("Value")

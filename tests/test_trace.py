@@ -59,6 +59,14 @@ SAMPLES = [
     (f"{P}/wpaxos.Accepted", {"Key": 0, "P2b": {"Ballot": 8590065667, "ID": "3.1", "Slot": 2}}),
     (f"{P}/wpaxos.Commit", {"Key": 5, "P3": {"Ballot": 8590065667, "Slot": 2, "Command": CMD_W}}),
     (f"{P}/wpaxos.LeaderChange", {"Key": 5, "To": "2.1", "From": "1.1", "Ballot": 8590065667}),
+    (f"{P}/epaxos.PreAccept", {"Ballot": 65537, "Replica": "1.1", "Slot": 3, "Command": CMD_W, "Seq": 4,
+                               "Dep": {"1.2": 2, "2.1": 7}}),
+    (f"{P}/epaxos.PreAcceptReply", {"Ballot": 65537, "Replica": "1.2", "Slot": 3, "Seq": 5, "Dep": {},
+                                    "Committed": {"1.1": 2, "1.2": -1, "2.1": 0}}),
+    (f"{P}/epaxos.Accept", {"Ballot": 65537, "Replica": "1.1", "Slot": 3, "Seq": 5, "Dep": {"1.2": 2}}),
+    (f"{P}/epaxos.AcceptReply", {"Ballot": 65537, "Replica": "2.1", "Slot": 3}),
+    (f"{P}/epaxos.Commit", {"Ballot": 65537, "Replica": "1.1", "Slot": 3, "Command": CMD_R, "Seq": 5,
+                            "Dep": {"1.2": 2}}),
 ]
 
 
@@ -154,8 +162,16 @@ def perkey_case(proto):
     return mk
 
 
+def epaxos_case(clusters=4, base=0):
+    cfg = abi.make_config(protocol=abi.EPAXOS, npz=[2, 2, 1], clusters=clusters, cluster_base=base, seed=11, keys=4,
+                          window=32, mbox_cap=32, max_delay=2)
+    wl = abi.make_workload(outstanding=5, target=list(range(5)), write_ppm=700_000)
+    fp = abi.make_fault_process(drop_ppm=1500, drop_len=10, slow_ppm=3000, slow_len=20, slow_min=1, slow_max=2)
+    return cfg, wl, fp
+
+
 CASES = {"paxos": paxos_case, "wpaxos": wpaxos_case, "abd": abd_case, "m2paxos": perkey_case(abi.M2PAXOS),
-         "kpaxos": perkey_case(abi.KPAXOS)}
+         "kpaxos": perkey_case(abi.KPAXOS), "epaxos": epaxos_case}
 KEEP = lambda t: t[:11] + t[12:14] + t[15:]   # replica state minus dropped and replies (the replay drops every send)
 
 
@@ -179,12 +195,12 @@ def replay_from_zero(backend, case, cluster=3, steps=150, tmpdir=None):
     return a, b, tr, streams, sa, sb
 
 
-@pytest.mark.parametrize("case", ["paxos", "wpaxos", "abd", "m2paxos", "kpaxos"])
+@pytest.mark.parametrize("case", ["paxos", "wpaxos", "abd", "m2paxos", "kpaxos", "epaxos"])
 def test_replay_oracle(case, tmp_path):
     a, b, tr, streams, sa, sb = replay_from_zero(OracleSim, case, tmpdir=str(tmp_path))
     assert len(tr["msgs"]) > 100 and len(streams) >= 4
     assert sa == sb
-    if case != "abd":
+    if case not in ("abd",):
         ia = [i.as_tuple() for i in a.read_instances(3, 1)]
         ib = [i.as_tuple() for i in b.read_instances(0, 1)]
         assert ia == ib
@@ -245,7 +261,7 @@ def test_read_inbox_parity_gpu(case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["paxos", "wpaxos", "abd", "m2paxos", "kpaxos"])
+@pytest.mark.parametrize("case", ["paxos", "wpaxos", "abd", "m2paxos", "kpaxos", "epaxos"])
 def test_replay_gpu(case):
     """Capture on the GPU, gob export and import, replay on the GPU: the replayed
     cluster retraces the captured one, and both equal the oracle's."""
