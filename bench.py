@@ -371,6 +371,13 @@ def main():
             out["roofline"]["traffic"] = tr["bytes_per_launch"]
             out["roofline"]["traffic_source"] = tr["source"]
             out["roofline"]["traffic_window"] = tr["window"]
+        try:   # the achievable HBM bandwidth on this part (tools/probe/copy_bw.hip), beside the spec peak
+            cb = json.load(open(os.path.join(ROOT, "profiles", "r2y", "copy_bw.json")))
+            out["roofline"]["measured_copy_peak"] = {"value": cb["copy_GBps"], "read_only": cb["read_GBps"],
+                                                     "frac_of_it": achieved / cb["copy_GBps"],
+                                                     "source": "profiles/r2y/copy_bw.json"}
+        except (OSError, ValueError, KeyError):
+            pass
         if lin is not None:
             out["linearizability"] = lin
         if not args.no_cpu_baseline:
