@@ -349,8 +349,8 @@ __device__ __forceinline__ void handle_request(const Params& P, Rep<NT>& x, uint
 // the first replica to reach digest checkpoint k records it, every later one
 // compares (a 64-bit CAS, so concurrent arrivals in one step agree on who was
 // first; whether some pair disagrees does not depend on that order).
-__device__ __forceinline__ void agree_arrive_body(unsigned long long* a, uint32_t* st0, size_t sstride, uint32_t k,
-                                                  uint64_t digest) {
+static __device__ __noinline__ void agree_arrive(unsigned long long* a, uint32_t* st0, size_t sstride, uint32_t k,
+                                         uint64_t digest) {
   const unsigned long long want = ((unsigned long long)k << 40) | ((digest ^ (digest >> 24)) & 0xFFFFFFFFFFull);
   unsigned long long v = atomicCAS(a, 0ull, want);
   uint32_t st = 0;                                       // 0: first to arrive, recorded
@@ -364,18 +364,6 @@ __device__ __forceinline__ void agree_arrive_body(unsigned long long* a, uint32_
   }
   if (st == ST_AGB) st0[ST_AGC * sstride] += 1;          // a mismatch was compared too
   if (st) st0[st * sstride] += 1;
-}
-// Inlined where it pays (A/B r2: config 2 +1%, config 5 +4%), a call in the
-// 9-replica Multi-Paxos kernel (config 4 -3% inlined)
-static __device__ __noinline__ void agree_arrive_call(unsigned long long* a, uint32_t* st0, size_t sstride,
-                                                      uint32_t k, uint64_t digest) {
-  agree_arrive_body(a, st0, sstride, k, digest);
-}
-template <int NT>
-__device__ __forceinline__ void agree_arrive(const Rep<NT>& x, unsigned long long* a, uint32_t* st0, size_t sstride,
-                                             uint32_t k, uint64_t digest) {
-  if (NT == 9 && !hbm_log(x)) agree_arrive_call(a, st0, sstride, k, digest);
-  else agree_arrive_body(a, st0, sstride, k, digest);
 }
 
 // Database.Execute (db.go:103-114) when replicas keep the KV: a write's value
@@ -414,7 +402,7 @@ __device__ __forceinline__ void paxos_exec(const Params& P, Rep<NT>& x) {     //
       P.ck_d[ci] = x.digest;
       if (P.AR) {
         const uint32_t kk = (uint32_t)x.execute / CKI;
-        agree_arrive<NT>(x, &P.agr[((size_t)(kk % P.AR) * P.NK + x.key) * P.C + x.c], &P.stats[rc(P, x.r, x.c)],
+        agree_arrive(&P.agr[((size_t)(kk % P.AR) * P.NK + x.key) * P.C + x.c], &P.stats[rc(P, x.r, x.c)],
                      (size_t)P.N * P.C, kk, x.digest);
       }
     }
