@@ -322,6 +322,7 @@ def capture(sim, cluster, steps):
     N = sim.N
     out = []
     t0 = sim.stats().steps
+    wl = sim.wl
     for k in range(steps):
         t = t0 + k
         for dst in range(N):
@@ -329,6 +330,11 @@ def capture(sim, cluster, steps):
             by_src = {}
             for r in recs:
                 by_src.setdefault(r[0], []).append(r)
+            # a worker starting at this step (paxisim_workload.start_step) sends its first
+            # request during the step, behind the ones already queued: not in the inbox yet
+            for w in range(wl.outstanding):
+                if t > 0 and wl.start_step[w] == t and wl.target[w] == dst:
+                    by_src.setdefault(N, []).append((N, T_REQUEST, 0, 0, 1 + w))
             for src in sorted(by_src):
                 for m in _split(by_src[src]):
                     out.append((t, src, dst, m))

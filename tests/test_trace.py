@@ -293,3 +293,30 @@ def test_deliver_into_frozen_cluster_gpu():
     g.step(40)
     o.step(40)
     assert [s.as_tuple() for s in g.read_state()] == [s.as_tuple() for s in o.read_state()]
+
+
+@pytest.mark.parametrize("config", [2, 4, 5])
+def test_trace_cli_roundtrip_oracle(config, tmp_path):
+    """tools/trace_cli.py: capture a BASELINE config's cluster to gob files, then
+    replay them from the files alone (the oracle stands in for the GPU here)."""
+    import argparse
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import trace_cli
+    d = str(tmp_path)
+    trace_cli.capture(argparse.Namespace(config=config, cluster=5, clusters=8, steps=120, crash_step=40, out=d),
+                      backend=OracleSim)
+    assert trace_cli.replay(argparse.Namespace(dir=d), backend=OracleSim)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", [2, 4, 5])
+def test_trace_cli_roundtrip_gpu(config, tmp_path):
+    """tools/trace_cli.py on the HIP path: capture and replay on the GPU."""
+    import argparse
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import trace_cli
+    d = str(tmp_path)
+    trace_cli.capture(argparse.Namespace(config=config, cluster=5, clusters=70, steps=150, crash_step=40, out=d))
+    assert trace_cli.replay(argparse.Namespace(dir=d))
