@@ -186,6 +186,16 @@ class Reader:
         return ~(u >> 1) if u & 1 else u >> 1
 
 
+def _float(u: int) -> float:
+    import struct
+    return struct.unpack("<d", u.to_bytes(8, "big"))[0]   # the uint holds the bytes in reverse order
+
+
+def enc_float(x: float) -> bytes:
+    import struct
+    return enc_uint(int.from_bytes(struct.pack("<d", x), "big"))
+
+
 # ---- type registry: ids as a fresh Go process hands them out ----------------
 class TypeIds:
     """Process-global type ids (encoding/gob type.go: nextId).  One instance
@@ -465,6 +475,11 @@ class Decoder:
             return m.uint()
         if tid == BOOL:
             return m.uint() != 0
+        if tid == FLOAT:                                  # float64 bits, byte-reversed, as a uint
+            return _float(m.uint())
+        if tid == COMPLEX:
+            re = _float(m.uint())
+            return complex(re, _float(m.uint()))
         if tid == STRING:
             return m.take(m.uint()).decode()
         if tid == BYTES:

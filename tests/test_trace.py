@@ -29,6 +29,9 @@ def test_gob_primitives_match_documentation():
         assert gob.Reader(bytes.fromhex(h)).int() == v
     for v, h in k["string"]:
         assert gob.enc_bytes(v.encode()).hex() == h
+    for v, h in k["float"]:
+        assert gob.enc_float(v).hex() == h
+        assert gob._float(gob.Reader(bytes.fromhex(h)).uint()) == v
 
 
 def test_gob_point_example():
