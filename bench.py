@@ -125,10 +125,11 @@ def measured_traffic(args, kernel, mbox, bid):
     """HBM bytes per launch from the PMC passes of tools/traffic.sh (committed as
     profiles/traffic_config<c>.json), attached when the record was measured on
     this build (source fingerprint) and this workload (kernel, clusters, window,
-    mailbox, launch size).  The simulation is seeded, so a launch at a given
-    simulated step moves the same bytes in every run; the record names the
-    bench window (warmup, steps) it averaged.  Counters cannot be read from
-    inside this process."""
+    mailbox, launch size) over this bench window (warmup, steps): the
+    simulation is seeded, so a launch at a given simulated step moves the same
+    bytes in every run, but bytes per launch change along the run (a ~1,200-step
+    ramp, then clusters dying), so a record of another window is not attached.
+    Counters cannot be read from inside this process."""
     path = os.path.join(ROOT, "profiles", f"traffic_config{args.config}.json")
     try:
         t = json.load(open(path))
@@ -136,7 +137,8 @@ def measured_traffic(args, kernel, mbox, bid):
         return None
     same = (t.get("kernel") == kernel and t.get("clusters_per_gpu") == args.clusters
             and t.get("sim_steps_per_step") == args.sim_steps and t.get("window") == args.window
-            and t.get("mbox_cap") == mbox and t.get("build_id") == bid)
+            and t.get("mbox_cap") == mbox and t.get("build_id") == bid
+            and t.get("warmup") == args.warmup and t.get("steps") == args.steps)
     if not same:
         return None
     return {"bytes_per_launch": t["bytes_per_launch"], "source": os.path.relpath(path, ROOT),

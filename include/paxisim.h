@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PAXISIM_ABI_VERSION 11
+#define PAXISIM_ABI_VERSION 12
 
 #define PAXISIM_MAX_N        16  /* replicas per cluster (ack masks are u16) */
 #define PAXISIM_MAX_ZONES    16
@@ -416,6 +416,13 @@ int  paxisim_read_kv(paxisim* h, uint64_t cluster, uint32_t replica, uint32_t* v
  * identical either way; this reports how many clusters the
  * step kernels still visit. */
 int  paxisim_active_clusters(paxisim* h, uint64_t* active);
+
+/* Per local cluster of [cluster_lo, cluster_lo+n): PAXISIM_STEPPED if the step
+ * kernels still visit it, else the step at which it was frozen at its fixed
+ * point.  Diagnostics for sampling parity checks; the state
+ * of a cluster does not depend on it. */
+#define PAXISIM_STEPPED 0xFFFFFFFFu
+int  paxisim_read_activity(paxisim* h, uint64_t cluster_lo, uint64_t n, uint32_t* frozen_at);
 
 /* Bytes of device memory held by the handle. */
 int  paxisim_device_bytes(paxisim* h, uint64_t* bytes);

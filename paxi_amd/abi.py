@@ -6,7 +6,7 @@ structs, so the two speak exactly the same ABI.
 """
 import ctypes as C
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 MAX_N = 16
 MAX_ZONES = 16
 MAX_WORKERS = 32

@@ -1,227 +1,425 @@
-// lin_kernel.h — History.Linearizable on gfx950 (history.go:55-71).
+// lin_kernel.h — History.Linearizable on gfx950 (history.go:55-71), no size cap.
 //
-// One thread checks one (cluster, key) partition of the completed-operation
-// history with the reference's graph algorithm, checker.go:69-104:
-//   ops sorted by start (stable); add() draws happens-before edges into each
-//   new vertex; a read looks ahead for concurrent writes, is merged into the
-//   write whose value it returned, and a cycle in the graph is an anomaly,
-//   after which the cycle's edges u->v with u.start > v.end are removed.
-// Vertex iteration is in insertion order (Go's map order is random; the
-// oracle uses the same insertion order).  The graph is a
-// 128x128 bit matrix; partitions with more than LIN_MAXV operations are
-// skipped and counted.  The recursive DFS of lib/graph.go:180-193 becomes an
-// explicit stack.  Workspace is per thread in HBM, field-major so that the
-// threads of a wave touch consecutive words.
+// The reference's checker (checker.go:69-104, lib/graph.go:180-232) runs on
+// every (cluster, key) partition of the completed-operation history:
+//   ops stable-sorted by start (sort.Sort(byTime)); add() draws happens-before
+//   edges into each new vertex; a read looks ahead for concurrent writes, is
+//   merged into the first vertex holding the value it returned, and Cycle()
+//   (a DFS over the vertices) reports an anomaly, after which the edges u->v
+//   with u.start > v.end among the DFS path's vertices are removed.
+// Vertices are iterated in insertion order where Go ranges over a map (the
+// oracle does the same), so a vertex is named by its insertion
+// number and "the first vertex in insertion order" is the lowest set bit.
+//
+// One wave checks one partition.  The adjacency matrix is a bit matrix with
+// one row of nw = ceil(cap/64) u64 words per vertex; bit sets that a DFS or a
+// search reads whole (present, gray, black, reach frontier) are spread one
+// word per lane (lane w holds word w), so a row scan is one load per lane and
+// a ballot.  Per read the wave pays O(n/64) for add/match/merge; Cycle() runs
+// only when the graph can hold a cycle:
+//   - add() gives the new vertex only incoming edges, so it never closes one;
+//   - merge(read, w) adds edges s->w, so an acyclic graph gains a cycle iff w
+//     reaches itself afterwards: a breadth-first reach from w over the rows;
+//   - after an anomaly the graph may still be cyclic, and then Cycle() runs at
+//     every read until it finds none, as in the reference.
+// When a cycle exists the exact insertion-order DFS runs, so the removed
+// edges are exactly the reference's.
+//
+// lin_cluster_kernel: one workgroup per cluster.  Its LIN_LW waves read the
+// cluster's history once (a pass over the key words, then one over the ops)
+// and write it to an HBM stage grouped by key, each key in canonical order
+// (replica 0's ops, then replica 1's, ... each in completion order: per-wave
+// counts and a stable ballot-ranked placement); then they take the keys in
+// turn and check partitions of up to LIN_SMAX ops in LDS.  Larger ones go to
+// a list that lin_big_kernel checks with the same code on an HBM scratch.
 #pragma once
 #include "paxisim_dev.h"
 
 namespace pxs {
 
-constexpr uint32_t LIN_MAXV = 128;
-constexpr uint32_t LIN_WORDS = LIN_MAXV / 64;   // u64 words per bit row
+constexpr uint32_t LIN_LW = 4;             // waves per cluster workgroup
+constexpr uint32_t LIN_SMAX = 128;         // partitions checked in LDS by the cluster kernel
+constexpr uint16_t LIN_NOV = 0xFFFFu;      // sorted op not (yet) a vertex
+enum { LIN_ANOM = 0, LIN_OPS, LIN_BIG, LIN_NMAX, LIN_PARTS, LIN_NOUT = 8 };
 
-struct LinWs {
-  uint64_t* adj;     // [LIN_MAXV][LIN_WORDS][T]
-  uint32_t* vin;     // [LIN_MAXV][T] write value (input)
-  uint32_t* vout;    // [LIN_MAXV][T] read value (output)
-  uint32_t* vstart;  // [LIN_MAXV][T]
-  uint32_t* vend;    // [LIN_MAXV][T]
-  uint32_t* vw;      // [LIN_MAXV][T] 1 = write (has input), 0 = read (has output)
-  uint32_t* order;   // [LIN_MAXV][T] insertion order
-  uint32_t* stk;     // [LIN_MAXV][T] DFS stack: vertex | next order index << 16
-  uint64_t T;
+// A wave's scratch for one partition of capacity cap = 64 * nw ops.
+struct LinScratch {
+  uint4* ops;        // [cap] sorted by start: {key | write << 31, value, start, end (refined)}
+  uint16_t* vid;     // [cap] sorted index -> vertex (insertion number) or LIN_NOV
+  uint16_t* opv;     // [cap] vertex -> sorted index
+  uint32_t* vst;     // [cap] vertex start
+  uint32_t* ven;     // [cap] vertex end (refined by merges)
+  uint32_t* vvl;     // [cap] vertex value | write << 31
+  uint32_t* stk;     // [cap] DFS stack: vertex | resume position << 16
+  uint64_t* rows;    // [cap][nw] successor bit rows
+  uint32_t nw;
 };
+__host__ __device__ inline size_t lin_scratch_bytes(uint32_t nw, bool) {
+  const size_t cap = 64u * (size_t)nw;
+  return cap * (16u + 2u + 2u + 4u * 4u) + cap * nw * 8u;
+}
+__device__ inline LinScratch lin_scratch(uint8_t* p, uint32_t nw, bool) {
+  const size_t cap = 64u * (size_t)nw;
+  LinScratch s;
+  s.rows = reinterpret_cast<uint64_t*>(p); p += cap * nw * 8u;
+  s.ops = reinterpret_cast<uint4*>(p); p += cap * 16u;
+  s.vst = reinterpret_cast<uint32_t*>(p); p += cap * 4u;
+  s.ven = reinterpret_cast<uint32_t*>(p); p += cap * 4u;
+  s.vvl = reinterpret_cast<uint32_t*>(p); p += cap * 4u;
+  s.stk = reinterpret_cast<uint32_t*>(p); p += cap * 4u;
+  s.vid = reinterpret_cast<uint16_t*>(p); p += cap * 2u;
+  s.opv = reinterpret_cast<uint16_t*>(p);
+  s.nw = nw;
+  return s;
+}
 
-struct Bits {
-  uint64_t w[LIN_WORDS];
-  __device__ __forceinline__ bool get(uint32_t i) const {
-    bool b = false;
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+// word w of a lane-distributed bit set (wave-uniform w)
+__device__ __forceinline__ uint64_t mword(uint64_t m, uint32_t w) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, (int)w);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(m >> 32), (int)w);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ bool mbit(uint64_t m, uint32_t v) { return (mword(m, v >> 6) >> (v & 63u)) & 1u; }
+__device__ __forceinline__ uint64_t mset(uint64_t m, uint32_t v) {
+  return lane_id() == (v >> 6) ? m | (1ull << (v & 63u)) : m;
+}
+__device__ __forceinline__ uint64_t mclr(uint64_t m, uint32_t v) {
+  return lane_id() == (v >> 6) ? m & ~(1ull << (v & 63u)) : m;
+}
+__device__ __forceinline__ uint64_t or_reduce(uint64_t v) {
 #pragma unroll
-    for (uint32_t k = 0; k < LIN_WORDS; k++) b |= (k == (i >> 6)) && ((w[k] >> (i & 63u)) & 1u);
-    return b;
-  }
-  __device__ __forceinline__ void set(uint32_t i) {
-#pragma unroll
-    for (uint32_t k = 0; k < LIN_WORDS; k++)
-      if (k == (i >> 6)) w[k] |= 1ull << (i & 63u);
-  }
-  __device__ __forceinline__ void clr(uint32_t i) {
-#pragma unroll
-    for (uint32_t k = 0; k < LIN_WORDS; k++)
-      if (k == (i >> 6)) w[k] &= ~(1ull << (i & 63u));
-  }
-  __device__ __forceinline__ void zero() {
-#pragma unroll
-    for (uint32_t k = 0; k < LIN_WORDS; k++) w[k] = 0;
-  }
-};
+  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ uint32_t first_lane(uint64_t ballot) { return (uint32_t)__builtin_ctzll(ballot); }
 
-struct Lin {
-  const LinWs& ws;
-  uint64_t tid;
-  uint32_t n, norder;
-  Bits present;
-  __device__ Lin(const LinWs& w, uint64_t t) : ws(w), tid(t), n(0), norder(0) { present.zero(); }
-  __device__ __forceinline__ size_t at(uint32_t v) const { return (size_t)v * ws.T + tid; }
-  __device__ __forceinline__ size_t adj_at(uint32_t v, uint32_t k) const {
-    return ((size_t)v * LIN_WORDS + k) * ws.T + tid;
+// The checker over one partition held in s.ops[0, n) (sorted).  Returns the
+// number of anomalous reads (checker.go:97: len(anomaly)).  Lanes write what
+// other lanes read next (rows, vertex fields, the DFS stack): LDS serves one
+// wave's accesses in order; with the scratch in HBM (G) a fence orders them.
+template <bool G>
+struct LinCheck {
+  LinScratch s;
+  uint32_t n, nv;       // ops, vertices inserted so far
+  uint64_t present;     // lane-distributed vertex set
+  uint64_t writes;      // lane-distributed: vertices that are writes (have an input)
+  __device__ __forceinline__ void sync() const {
+    if (G) __threadfence_block();
   }
-  __device__ __forceinline__ bool edge(uint32_t u, uint32_t v) const {
-    return (ws.adj[adj_at(u, v >> 6)] >> (v & 63u)) & 1u;
+  __device__ __forceinline__ bool hb_ops(uint32_t a, uint32_t b) const {   // operation.go:12-14 on sorted ops
+    return s.ops[a].w < s.ops[b].z;
   }
-  __device__ __forceinline__ void set_edge(uint32_t u, uint32_t v) { ws.adj[adj_at(u, v >> 6)] |= 1ull << (v & 63u); }
-  __device__ __forceinline__ void clr_edge(uint32_t u, uint32_t v) { ws.adj[adj_at(u, v >> 6)] &= ~(1ull << (v & 63u)); }
-  __device__ __forceinline__ bool happen_before(uint32_t a, uint32_t b) const {   // operation.go:12-14
-    return ws.vend[at(a)] < ws.vstart[at(b)];
+  // checker.add (checker.go:21-33): edges v -> o from every vertex that happened before o
+  __device__ void add(uint32_t o) {
+    if (s.vid[o] != LIN_NOV) return;                     // already in graph from lookahead
+    const uint4 op = s.ops[o];
+    const uint32_t id = nv++;
+    if (lane_id() == 0) {
+      s.vid[o] = (uint16_t)id;
+      s.opv[id] = (uint16_t)o;
+      s.vst[id] = op.z;
+      s.ven[id] = op.w;
+      s.vvl[id] = op.y;
+    }
+    for (uint32_t w = lane_id(); w < s.nw; w += 64u) s.rows[(size_t)id * s.nw + w] = 0;
+    present = mset(present, id);
+    if (op.x >> 31) writes = mset(writes, id);
+    for (uint32_t b = 0; b < id; b += 64u) {             // the new vertex is not before itself
+      const uint32_t v = b + lane_id();
+      const uint64_t pw = mword(present, b >> 6);
+      if (v < id && ((pw >> (v & 63u)) & 1u) && s.ven[v] < op.z)
+        s.rows[(size_t)v * s.nw + (id >> 6)] |= 1ull << (id & 63u);
+    }
+    sync();
   }
-  __device__ __forceinline__ void add_vertex(uint32_t v) {
-    if (present.get(v)) return;
-    present.set(v);
-    ws.order[at(norder++)] = v;
+  // graph.Remove (graph.go:36-48)
+  __device__ void remove(uint32_t r) {
+    present = mclr(present, r);
+    for (uint32_t w = lane_id(); w < s.nw; w += 64u) s.rows[(size_t)r * s.nw + w] = 0;
+    for (uint32_t b = 0; b < nv; b += 64u) {
+      const uint32_t v = b + lane_id();
+      if (v < nv) s.rows[(size_t)v * s.nw + (r >> 6)] &= ~(1ull << (r & 63u));
+    }
+    sync();
   }
-  __device__ __forceinline__ void chk_add(uint32_t o) {                            // checker.go:21-33
-    if (present.get(o)) return;
-    add_vertex(o);
-    for (uint32_t k = 0; k < norder; k++) {
-      const uint32_t v = ws.order[at(k)];
-      if (happen_before(v, o)) set_edge(v, o);
+  // match (checker.go:44-52): the first vertex whose input equals the read's
+  // output (a read has no input: only writes match a read's value)
+  __device__ uint32_t match(uint32_t out) const {
+    for (uint32_t b = 0; b < nv; b += 64u) {
+      const uint32_t v = b + lane_id();
+      const uint64_t pw = mword(present & writes, b >> 6);
+      const bool hit = v < nv && ((pw >> (v & 63u)) & 1u) && s.vvl[v] == out;
+      const uint64_t m = __ballot(hit);
+      if (m) return b + first_lane(m);
+    }
+    return LIN_NOV;
+  }
+  // merge (checker.go:55-67): the write inherits the read's incoming edges
+  __device__ void merge(uint32_t r, uint32_t m) {
+    for (uint32_t b = 0; b < nv; b += 64u) {
+      const uint32_t v = b + lane_id();
+      if (v < nv && v != m && ((s.rows[(size_t)v * s.nw + (r >> 6)] >> (r & 63u)) & 1u))
+        s.rows[(size_t)v * s.nw + (m >> 6)] |= 1ull << (m & 63u);
+    }
+    if (lane_id() == 0 && s.ven[r] < s.ven[m]) {         // refine response time of the merged vertex
+      s.ven[m] = s.ven[r];
+      s.ops[s.opv[m]].w = s.ven[r];
+    }
+    sync();
+    remove(r);
+  }
+  // Does m reach itself?  Breadth-first over the rows, one word a lane.
+  __device__ bool reaches_self(uint32_t m) const {
+    uint64_t R = mset(0ull, m), F = R;
+    for (;;) {
+      uint64_t nx = 0;
+      bool any = false;
+      for (uint32_t w = 0; w < s.nw; w++) {
+        uint64_t acc = 0;
+        for (uint32_t b = 0; b < nv; b += 64u) {
+          const uint64_t fw = mword(F, b >> 6);
+          if (!fw) continue;
+          const uint32_t v = b + lane_id();
+          if ((fw >> (v & 63u)) & 1u) acc |= s.rows[(size_t)v * s.nw + w];
+        }
+        acc = or_reduce(acc);
+        if (w == (m >> 6) && ((acc >> (m & 63u)) & 1u)) return true;
+        if (lane_id() == w) nx = acc;
+      }
+      nx &= present & ~R;
+      any = __ballot(nx != 0) != 0;
+      if (!any) return false;
+      R |= nx;
+      F = nx;
     }
   }
-  __device__ __forceinline__ void remove(uint32_t v) {                             // graph.go:36-48
-    if (!present.get(v)) return;
-    present.clr(v);
-    for (uint32_t k = 0; k < LIN_WORDS; k++) ws.adj[adj_at(v, k)] = 0;
-    uint32_t j = 0;
-    for (uint32_t k = 0; k < norder; k++) {
-      const uint32_t u = ws.order[at(k)];
-      clr_edge(u, v);
-      if (u != v) ws.order[at(j++)] = u;
-    }
-    norder = j;
-  }
-  // Cycle() (graph.go:212-232): returns true and leaves `gray` = the DFS stack
-  __device__ bool cycle(Bits& gray) {
-    Bits black;
-    black.zero();
-    gray.zero();
-    for (uint32_t s = 0; s < norder; s++) {
-      const uint32_t root = ws.order[at(s)];
-      if (gray.get(root) || black.get(root)) continue;
-      uint32_t sp = 0;
-      gray.set(root);
-      ws.stk[at(sp++)] = root;
-      while (sp) {                                                                  // visit(): graph.go:180-193
-        const uint32_t top = ws.stk[at(sp - 1)];
-        const uint32_t v = top & 0xFFFFu;
-        uint32_t k = top >> 16;
-        uint32_t u = 0;
-        bool next = false;
-        for (; k < norder; k++) {
-          u = ws.order[at(k)];
-          if (edge(v, u) && !black.get(u)) { next = true; break; }
+  // Cycle() (graph.go:212-232): DFS from each white vertex in insertion order,
+  // visit (180-193) walking successors in insertion order; on a back edge the
+  // gray vertices (the DFS path) are returned in `gray`.
+  __device__ bool cycle(uint64_t& gray) const {
+    uint64_t black = 0;
+    gray = 0;
+    for (uint32_t rb = 0; rb < nv; rb += 64u) {
+      uint64_t roots = mword(present & ~black, rb >> 6);
+      while (roots) {
+        const uint32_t root = rb + (uint32_t)__builtin_ctzll(roots);
+        roots &= roots - 1u;
+        if (mbit(black, root)) continue;                 // reached from an earlier root
+        uint32_t sp = 0, v = root, k = 0;
+        gray = mset(gray, root);
+        for (;;) {
+          // the first successor u >= k of v that is not black
+          const uint32_t w = lane_id();
+          uint64_t c = 0;
+          if (w < s.nw && w * 64u + 63u >= k) {
+            c = s.rows[(size_t)v * s.nw + w] & ~black;
+            if (w * 64u < k) c &= ~0ull << (k - w * 64u);
+          }
+          const uint64_t bl = __ballot(c != 0);
+          if (!bl) {                                     // v done: black, back to its parent
+            gray = mclr(gray, v);
+            black = mset(black, v);
+            if (sp == 0) break;
+            const uint32_t top = s.stk[--sp];
+            v = top & 0xFFFFu;
+            k = top >> 16;
+            continue;
+          }
+          const uint32_t f = first_lane(bl);
+          const uint64_t cw = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)c, (int)f) |
+                              ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(c >> 32), (int)f) << 32);
+          const uint32_t u = f * 64u + (uint32_t)__builtin_ctzll(cw);
+          if (mbit(gray, u)) return true;
+          if (lane_id() == 0) s.stk[sp] = v | ((u + 1u) << 16);
+          sync();
+          sp++;
+          gray = mset(gray, u);
+          v = u;
+          k = 0;
         }
-        if (!next) {
-          gray.clr(v);
-          black.set(v);
-          sp--;
-          continue;
-        }
-        ws.stk[at(sp - 1)] = v | ((k + 1u) << 16);
-        if (gray.get(u)) return true;
-        gray.set(u);
-        ws.stk[at(sp++)] = u;
       }
     }
     return false;
   }
+  // checker.go:93-100: remove the edges u->v between gray vertices with u.start > v.end
+  __device__ void cut(uint64_t gray) {
+    for (uint32_t b = 0; b < nv; b += 64u) {
+      const uint32_t u = b + lane_id();
+      const uint64_t gw = mword(gray, b >> 6);
+      if (u >= nv || !((gw >> (u & 63u)) & 1u)) continue;
+      const uint32_t su = s.vst[u];
+      for (uint32_t w = 0; w < s.nw; w++) {
+        uint64_t e = s.rows[(size_t)u * s.nw + w] & mword(gray, w), keep = ~0ull;
+        while (e) {
+          const uint32_t t = (uint32_t)__builtin_ctzll(e);
+          e &= e - 1u;
+          if (su > s.ven[w * 64u + t]) keep &= ~(1ull << t);
+        }
+        if (keep != ~0ull) s.rows[(size_t)u * s.nw + w] &= keep;
+      }
+    }
+    sync();
+  }
+  // checker.linearizable (checker.go:69-104) over the sorted ops
+  __device__ uint32_t run() {
+    nv = 0;
+    present = writes = 0;
+    for (uint32_t i = lane_id(); i < n; i += 64u) s.vid[i] = LIN_NOV;
+    sync();
+    bool maybe_cyclic = false;
+    uint32_t anomalies = 0;
+    for (uint32_t i = 0; i < n; i++) {
+      add(i);
+      const uint4 o = s.ops[i];
+      if (o.x >> 31) continue;                           // a write: nothing more
+      for (uint32_t j = i + 1; j < n && !hb_ops(i, j) && !hb_ops(j, i); j++)   // look ahead
+        if (s.ops[j].x >> 31) add(j);                    // concurrent writes
+      const uint32_t r = s.vid[i];
+      const uint32_t m = match(o.y);
+      if (m != LIN_NOV) merge(r, m);
+      bool cyc = false;
+      uint64_t gray = 0;
+      if (maybe_cyclic) cyc = cycle(gray);
+      else if (m != LIN_NOV && reaches_self(m)) cyc = cycle(gray);
+      if (cyc) {
+        anomalies++;
+        cut(gray);
+        uint64_t g2;
+        maybe_cyclic = cycle(g2);                        // still cyclic: Cycle() at every read
+      } else {
+        maybe_cyclic = false;
+      }
+    }
+    return anomalies;
+  }
 };
 
-// grid: one thread per (cluster, key) of clusters [c0, c0+nc)
-__global__ void lin_kernel(Params P, LinWs ws, uint64_t c0, uint64_t nc, uint64_t* out) {
-  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t anomalies = 0, checked = 0, skipped = 0;
-  if (tid < nc * P.keys) {
-    const uint64_t c = c0 + tid / P.keys;
-    const uint32_t key = (uint32_t)(tid % P.keys);
-    Lin g(ws, tid);
-    // gather the partition in canonical order, then stable-sort by start (sort.Sort(byTime))
-    uint32_t n = 0;
-    bool over = false;
-    for (uint32_t r = 0; r < P.N; r++) {
-      const uint32_t len = P.execute[rc(P, r, c)];
-      const uint4* h = &P.hist[((size_t)r * P.C + c) * P.H];
-      for (uint32_t j = 0; j < len; j++) {
-        const uint4 o = h[j];
-        if ((o.x & 0x7FFFFFFFu) != key) continue;
-        if (n == LIN_MAXV) { over = true; break; }
-        const uint32_t w = o.x >> 31;
-        uint32_t p = n++;
-        while (p > 0 && ws.vstart[g.at(p - 1)] > o.z) {          // insertion sort: stable
-          ws.vin[g.at(p)] = ws.vin[g.at(p - 1)];
-          ws.vout[g.at(p)] = ws.vout[g.at(p - 1)];
-          ws.vstart[g.at(p)] = ws.vstart[g.at(p - 1)];
-          ws.vend[g.at(p)] = ws.vend[g.at(p - 1)];
-          ws.vw[g.at(p)] = ws.vw[g.at(p - 1)];
-          p--;
-        }
-        ws.vin[g.at(p)] = w ? o.y : 0u;
-        ws.vout[g.at(p)] = w ? 0u : o.y;
-        ws.vstart[g.at(p)] = o.z;
-        ws.vend[g.at(p)] = o.w;
-        ws.vw[g.at(p)] = w;
-      }
-      if (over) break;
+// Stable sort of src[0, n) by start into s.ops (sort.Sort(byTime): ties keep
+// canonical order): each op's rank counts the ops before it.
+template <bool G>
+__device__ inline void lin_sort(const uint4* src, uint32_t n, LinScratch& s) {
+  for (uint32_t i = lane_id(); i < n; i += 64u) {
+    const uint4 o = src[i];
+    uint32_t rk = 0;
+    for (uint32_t j = 0; j < n; j++) {
+      const uint32_t sj = src[j].z;
+      rk += (sj < o.z || (sj == o.z && j < i)) ? 1u : 0u;
     }
-    if (over) {
-      skipped = 1;
-    } else if (n) {
-      checked = n;
-      for (uint32_t v = 0; v < n; v++)
-        for (uint32_t k = 0; k < LIN_WORDS; k++) ws.adj[g.adj_at(v, k)] = 0;
-      for (uint32_t i = 0; i < n; i++) {                          // checker.go:73-102
-        g.chk_add(i);
-        if (ws.vw[g.at(i)]) continue;                              // writes: nothing more
-        for (uint32_t j = i + 1; j < n && !g.happen_before(i, j) && !g.happen_before(j, i); j++)
-          if (ws.vw[g.at(j)]) g.chk_add(j);                        // look-ahead concurrent writes
-        int match = -1;                                            // match: checker.go:44-52
-        for (uint32_t k = 0; k < g.norder; k++) {
-          const uint32_t v = ws.order[g.at(k)];
-          if (ws.vw[g.at(v)] && ws.vin[g.at(v)] == ws.vout[g.at(i)]) { match = (int)v; break; }
-        }
-        if (match >= 0) {                                          // merge: checker.go:55-67
-          const uint32_t mw = (uint32_t)match;
-          for (uint32_t k = 0; k < g.norder; k++) {
-            const uint32_t s2 = ws.order[g.at(k)];
-            if (g.edge(s2, i) && s2 != mw) g.set_edge(s2, mw);
-          }
-          if (ws.vend[g.at(i)] < ws.vend[g.at(mw)]) ws.vend[g.at(mw)] = ws.vend[g.at(i)];
-          g.remove(i);
-        }
-        Bits gray;
-        if (g.cycle(gray)) {
-          anomalies++;
-          for (uint32_t a = 0; a < g.norder; a++) {
-            const uint32_t u = ws.order[g.at(a)];
-            if (!gray.get(u)) continue;
-            for (uint32_t b = 0; b < g.norder; b++) {
-              const uint32_t v = ws.order[g.at(b)];
-              if (gray.get(v) && g.edge(u, v) && ws.vstart[g.at(u)] > ws.vend[g.at(v)]) g.clr_edge(u, v);
-            }
-          }
-        }
+    s.ops[rk] = o;
+  }
+  if (G) __threadfence_block();
+}
+
+// Canonical op index -> its history record (replica-major; len[r] ops each).
+__device__ __forceinline__ const uint4* hist_at(const Params& P, uint64_t c, const uint32_t* len, uint32_t idx) {
+  uint32_t r = 0;
+  while (idx >= len[r]) idx -= len[r++];
+  return &P.hist[((size_t)r * P.C + c) * P.H + idx];
+}
+
+// grid: one workgroup (LIN_LW waves) per cluster c0 + blockIdx.x.  stage:
+// [grid][N*H] ops, the cluster's history grouped by key (its own region of
+// the launch's workspace).  Dynamic LDS: LIN_LW small-partition scratches.
+__global__ void __launch_bounds__(LIN_LW * 64) lin_cluster_kernel(Params P, uint64_t c0, uint4* stage_all,
+                                                                   unsigned long long* out, uint2* big) {
+  extern __shared__ uint4 lds_lin[];
+  __shared__ uint32_t len[PAXISIM_MAX_N];
+  __shared__ uint32_t cnt[LIN_LW][PAXISIM_MAX_KEYS];   // per wave slice, per key
+  __shared__ uint32_t koff[PAXISIM_MAX_KEYS + 1];
+  const uint64_t c = c0 + blockIdx.x;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t K = P.keys;
+  const uint32_t cap = P.N * P.H;
+  uint4* stage = stage_all + (size_t)blockIdx.x * cap;
+  uint8_t* wsp = reinterpret_cast<uint8_t*>(lds_lin) + wave * lin_scratch_bytes(LIN_SMAX / 64u, false);
+  if (threadIdx.x < P.N) len[threadIdx.x] = P.execute[rc(P, threadIdx.x, c)];
+  for (uint32_t k = threadIdx.x; k < LIN_LW * PAXISIM_MAX_KEYS; k += blockDim.x) (&cnt[0][0])[k] = 0;
+  __syncthreads();
+  uint32_t tot = 0;
+  for (uint32_t r = 0; r < P.N; r++) tot += len[r];
+  // pass 1: per-key counts of each wave's slice of the canonical sequence (key words only)
+  const uint32_t per = (tot + LIN_LW - 1u) / LIN_LW;
+  const uint32_t lo = wave * per < tot ? wave * per : tot, hi = lo + per < tot ? lo + per : tot;
+  for (uint32_t i = lo + lane_id(); i < hi; i += 64u) {
+    const uint32_t key = *reinterpret_cast<const uint32_t*>(hist_at(P, c, len, i)) & 0x7FFFFFFFu;
+    if (key < K) atomicAdd(&cnt[wave][key], 1u);       // (paxisim_history_load admits keys < K only)
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {                              // key-major, wave-minor exclusive scan
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < K; k++) {
+      koff[k] = acc;
+      for (uint32_t w = 0; w < LIN_LW; w++) {
+        const uint32_t v = cnt[w][k];
+        cnt[w][k] = acc;
+        acc += v;
       }
     }
+    koff[K] = acc;
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    anomalies += __shfl_down(anomalies, o, 64);
-    checked += __shfl_down(checked, o, 64);
-    skipped += __shfl_down(skipped, o, 64);
+  __syncthreads();
+  // pass 2: stable placement by key.  Each wave walks its slice in 64-op
+  // chunks; an op goes to its key's running offset for this wave plus its
+  // rank among the chunk's ops of that key (a ballot per distinct key).
+  for (uint32_t i0 = lo; i0 < hi; i0 += 64u) {
+    const uint32_t i = i0 + lane_id();
+    const uint4 o = i < hi ? *hist_at(P, c, len, i) : make_uint4(0u, 0u, 0u, 0u);
+    const bool act = i < hi && (o.x & 0x7FFFFFFFu) < K;
+    const uint32_t key = act ? (o.x & 0x7FFFFFFFu) : 0xFFFFFFFFu;
+    uint64_t todo = __ballot(act);
+    while (todo) {
+      const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)first_lane(todo));
+      const uint64_t m = __ballot(key == kk);
+      const uint32_t base = cnt[wave][kk];
+      if (key == kk) stage[base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = o;
+      __builtin_amdgcn_wave_barrier();
+      if (lane_id() == 0) cnt[wave][kk] = base + (uint32_t)__popcll(m);
+      todo &= ~m;
+    }
   }
-  if ((threadIdx.x & 63) == 0) {
-    if (anomalies) atomicAdd((unsigned long long*)&out[0], (unsigned long long)anomalies);
-    if (checked) atomicAdd((unsigned long long*)&out[1], (unsigned long long)checked);
-    if (skipped) atomicAdd((unsigned long long*)&out[2], (unsigned long long)skipped);
+  __threadfence_block();
+  __syncthreads();
+  // pass 3: the keys in turn, one wave each
+  unsigned long long anomalies = 0, ops = 0;
+  for (uint32_t k = wave; k < K; k += LIN_LW) {
+    const uint32_t n = koff[k + 1] - koff[k];
+    if (!n) continue;
+    ops += n;
+    if (n > LIN_SMAX) {                                // the big path
+      if (lane_id() == 0) {
+        const uint32_t slot = (uint32_t)atomicAdd(&out[LIN_BIG], 1ull);
+        big[slot] = make_uint2(blockIdx.x * cap + koff[k], n);
+        atomicMax(&out[LIN_NMAX], (unsigned long long)n);
+      }
+      continue;
+    }
+    LinCheck<false> g;
+    g.s = lin_scratch(wsp, LIN_SMAX / 64u, false);
+    g.n = n;
+    lin_sort<false>(stage + koff[k], n, g.s);
+    anomalies += g.run();
   }
+  if (lane_id() == 0) {
+    if (anomalies) atomicAdd(&out[LIN_ANOM], anomalies);
+    if (ops) atomicAdd(&out[LIN_OPS], ops);
+  }
+}
+
+// grid-stride over the big partitions {stage offset, ops}: one wave each,
+// scratch in HBM (slot = blockIdx.x), capacity 64 * nw ops.
+__global__ void __launch_bounds__(64) lin_big_kernel(const uint4* stage_all, const uint2* big, uint32_t nbig,
+                                                     uint8_t* ws, uint32_t nw, unsigned long long* out) {
+  const LinScratch s = lin_scratch(ws + (size_t)blockIdx.x * lin_scratch_bytes(nw, false), nw, false);
+  unsigned long long anomalies = 0;
+  for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
+    LinCheck<true> g;
+    g.s = s;
+    g.n = big[b].y;
+    lin_sort<true>(stage_all + big[b].x, g.n, g.s);
+    anomalies += g.run();
+  }
+  if (lane_id() == 0 && anomalies) atomicAdd(&out[LIN_ANOM], anomalies);
 }
 
 }  // namespace pxs

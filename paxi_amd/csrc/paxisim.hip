@@ -14,6 +14,7 @@
 #include <cstring>
 #include <new>
 #include <utility>
+#include <algorithm>
 #include <vector>
 
 #include "epaxos_kernel.h"
@@ -45,8 +46,8 @@ struct paxisim {
   paxisim_fault_process fp;
   Params P;
   uint32_t zone_of[PAXISIM_MAX_N], node_of[PAXISIM_MAX_N];
-  std::vector<paxisim_fault> faults;
-  paxisim_fault* d_faults = nullptr;
+  std::vector<DevFault> faults;
+  DevFault* d_faults = nullptr;
   void* arena = nullptr;
   size_t arena_bytes = 0;
   uint64_t* d_scratch = nullptr;   // reductions
@@ -65,6 +66,7 @@ struct paxisim {
   uint32_t last_cmp = 0;
   uint32_t late_until = 0;         // no compaction before every late worker has started
   uint32_t bound_host = 0;         // last bound read back (diagnostics)
+  uint64_t lin_big = 0, lin_nmax = 0;   // last linearizability scan: partitions above LIN_SMAX, largest
 };
 
 static inline size_t rc_host(const Params& P, uint32_t r, uint64_t c) { return (size_t)r * P.C + c; }
@@ -950,7 +952,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
       (e = hipMalloc(&h->d_scratch, sizeof(uint64_t) * 64)) != hipSuccess ||
       (e = hipMalloc(&h->d_cmp, sizeof(uint32_t) * ncmp)) != hipSuccess ||
       (e = hipMalloc(&h->d_pairs, sizeof(uint32_t) * 2 * (C / 2 + LANES))) != hipSuccess ||
-      (e = hipMalloc(&h->d_faults, sizeof(paxisim_fault) * PAXISIM_MAX_FAULTS)) != hipSuccess ||
+      (e = hipMalloc(&h->d_faults, sizeof(DevFault) * PAXISIM_MAX_FAULTS)) != hipSuccess ||
       (e = hipMemsetAsync(h->arena, 0, zero_bytes, h->stream)) != hipSuccess)
     rc1 = fail(PAXISIM_EDEVICE, "device setup failed: %s", hipGetErrorString(e));
   if (!rc1) {
@@ -985,8 +987,8 @@ extern "C" int paxisim_fault_add(paxisim* h, const paxisim_fault* f) {
   if (f->kind == PAXISIM_FAULT_SLOW && f->param > h->cfg.max_delay)
     return fail(PAXISIM_EINVAL, "slow delay exceeds max_delay");
   HIPCHK(hipSetDevice(h->cfg.device));
-  h->faults.push_back(*f);
-  HIPCHK(hipMemcpyAsync(h->d_faults, h->faults.data(), h->faults.size() * sizeof(paxisim_fault),
+  h->faults.push_back(dev_fault(*f));
+  HIPCHK(hipMemcpyAsync(h->d_faults, h->faults.data(), h->faults.size() * sizeof(DevFault),
                         hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   h->P.nfaults = (uint32_t)h->faults.size();
@@ -1079,6 +1081,29 @@ extern "C" int paxisim_active_clusters(paxisim* h, uint64_t* active) {
   HIPCHK(hipStreamSynchronize(h->stream));
   h->bound_host = bound;
   *active = bound;
+  return 0;
+}
+
+__global__ void activity_kernel(Params P, uint64_t lo, uint64_t n, uint32_t* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t s = slot_of(P, lo + i);
+  out[i] = s < *P.bound ? 0xFFFFFFFFu : P.frz[s];
+}
+
+extern "C" int paxisim_read_activity(paxisim* h, uint64_t lo, uint64_t n, uint32_t* frozen_at) {
+  if (!h || !frozen_at) return fail(PAXISIM_EINVAL, "null argument");
+  if (lo + n > h->cfg.clusters || lo + n < lo) return fail(PAXISIM_ERANGE, "cluster range");
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(h->cfg.device));
+  uint32_t* d = nullptr;
+  HIPCHK(hipMalloc(&d, n * sizeof(uint32_t)));
+  activity_kernel<<<(unsigned)((n + 255) / 256), 256, 0, h->stream>>>(h->P, lo, n, d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(frozen_at, d, n * sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(PAXISIM_EDEVICE, "read_activity: %s", hipGetErrorString(e));
   return 0;
 }
 
@@ -1386,7 +1411,7 @@ extern "C" int paxisim_history_load(paxisim* h, uint64_t cluster, uint32_t repli
   std::vector<uint4> tmp(n ? n : 1);
   for (uint32_t j = 0; j < n; j++) {
     const uint32_t* o = ops + 5 * (size_t)j;
-    if (o[0] > 0x7FFFFFFFu || o[1] > 1u) return fail(PAXISIM_EINVAL, "op %u: bad key or is_write", j);
+    if (o[0] >= h->P.keys || o[1] > 1u) return fail(PAXISIM_EINVAL, "op %u: bad key (keys = %u) or is_write", j, h->P.keys);
     tmp[j] = make_uint4(o[0] | (o[1] << 31), o[2], o[3], o[4]);
   }
   if (n)
@@ -1401,42 +1426,64 @@ extern "C" int paxisim_linearizable(paxisim* h, uint64_t* anomalies, uint64_t* o
   if (h->P.protocol != PAXISIM_ABD || h->P.H == 0)
     return fail(PAXISIM_EUNSUPP, "linearizability scan needs protocol ABD with history > 0");
   HIPCHK(hipSetDevice(h->cfg.device));
+  HIPCHK(hipStreamSynchronize(h->stream));
   const Params& P = h->P;
-  // per-thread workspace, one chunk of (cluster, key) partitions at a time
-  const uint64_t total = P.clusters * P.keys;
-  const uint64_t T = total < (1ull << 18) ? (total + 63) / 64 * 64 : (1ull << 18);
-  const size_t per = (size_t)LIN_MAXV * (LIN_WORDS * 8 + 7 * 4);
-  char* ws_mem = nullptr;
-  HIPCHK(hipMalloc(&ws_mem, per * T));
-  LinWs ws;
-  {
-    char* p = ws_mem;
-    ws.adj = reinterpret_cast<uint64_t*>(p); p += (size_t)LIN_MAXV * LIN_WORDS * 8 * T;
-    ws.vin = reinterpret_cast<uint32_t*>(p); p += (size_t)LIN_MAXV * 4 * T;
-    ws.vout = reinterpret_cast<uint32_t*>(p); p += (size_t)LIN_MAXV * 4 * T;
-    ws.vstart = reinterpret_cast<uint32_t*>(p); p += (size_t)LIN_MAXV * 4 * T;
-    ws.vend = reinterpret_cast<uint32_t*>(p); p += (size_t)LIN_MAXV * 4 * T;
-    ws.vw = reinterpret_cast<uint32_t*>(p); p += (size_t)LIN_MAXV * 4 * T;
-    ws.order = reinterpret_cast<uint32_t*>(p); p += (size_t)LIN_MAXV * 4 * T;
-    ws.stk = reinterpret_cast<uint32_t*>(p);
-    ws.T = T;
+  // clusters per launch: each gets a stage of N*H ops (its history grouped by key)
+  const size_t cap = (size_t)P.N * P.H;
+  const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(P.clusters, (2ull << 30) / (cap * sizeof(uint4))));
+  uint4* stage = nullptr;
+  uint2* big = nullptr;
+  unsigned long long* out = nullptr;
+  uint8_t* bws = nullptr;
+  size_t bws_bytes = 0;
+  const size_t nout = LIN_NOUT + 8;
+  auto cleanup = [&]() {
+    (void)hipFree(stage);
+    (void)hipFree(big);
+    (void)hipFree(out);
+    (void)hipFree(bws);
+  };
+  hipError_t e = hipMalloc(&stage, chunk * cap * sizeof(uint4));
+  if (e == hipSuccess) e = hipMalloc(&big, chunk * P.keys * sizeof(uint2));
+  if (e == hipSuccess) e = hipMalloc(&out, nout * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemsetAsync(out, 0, nout * sizeof(unsigned long long), h->stream);
+  const uint32_t lds = (uint32_t)(LIN_LW * lin_scratch_bytes(LIN_SMAX / 64u, false));
+  unsigned long long tot[LIN_NOUT] = {0};
+  for (uint64_t c0 = 0; e == hipSuccess && c0 < P.clusters; c0 += chunk) {
+    const uint64_t nc = std::min<uint64_t>(chunk, P.clusters - c0);
+    if ((e = hipMemsetAsync(out + LIN_BIG, 0, 2 * sizeof(unsigned long long), h->stream)) != hipSuccess) break;
+    lin_cluster_kernel<<<(unsigned)nc, LIN_LW * 64, lds, h->stream>>>(P, c0, stage, out, big);
+    unsigned long long bc[2] = {0, 0};
+    if ((e = hipGetLastError()) != hipSuccess) break;
+    if ((e = hipMemcpyAsync(bc, out + LIN_BIG, sizeof bc, hipMemcpyDeviceToHost, h->stream)) != hipSuccess) break;
+    if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) break;
+    if (bc[0]) {   // partitions above LIN_SMAX ops: one wave each, scratch in HBM
+      tot[LIN_BIG] += bc[0];
+      tot[LIN_NMAX] = std::max<unsigned long long>(tot[LIN_NMAX], bc[1]);
+      const uint32_t nw = (uint32_t)((bc[1] + 63u) / 64u);
+      const uint32_t waves = (uint32_t)std::min<unsigned long long>(bc[0], 2048);
+      const size_t need = (size_t)waves * lin_scratch_bytes(nw, true);
+      if (need > bws_bytes) {
+        (void)hipFree(bws);
+        bws = nullptr;
+        bws_bytes = 0;
+        if ((e = hipMalloc(&bws, need)) != hipSuccess) break;
+        bws_bytes = need;
+      }
+      lin_big_kernel<<<waves, 64, 0, h->stream>>>(stage, big, (uint32_t)bc[0], bws, nw, out);
+      if ((e = hipGetLastError()) != hipSuccess) break;
+    }
   }
-  hipError_t e = hipMemsetAsync(h->d_scratch, 0, 3 * sizeof(uint64_t), h->stream);
-  const uint64_t per_chunk = T / P.keys;
-  for (uint64_t c0 = 0; e == hipSuccess && c0 < P.clusters; c0 += per_chunk) {
-    const uint64_t nc = (P.clusters - c0) < per_chunk ? (P.clusters - c0) : per_chunk;
-    const uint64_t threads = nc * P.keys;
-    lin_kernel<<<(unsigned)((threads + 63) / 64), 64, 0, h->stream>>>(P, ws, c0, nc, h->d_scratch);
-    e = hipGetLastError();
-  }
-  uint64_t res[3] = {0, 0, 0};
-  if (e == hipSuccess) e = hipMemcpyAsync(res, h->d_scratch, sizeof res, hipMemcpyDeviceToHost, h->stream);
+  uint64_t res[LIN_NOUT] = {0};
+  if (e == hipSuccess) e = hipMemcpyAsync(res, out, sizeof res, hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-  (void)hipFree(ws_mem);
+  cleanup();
   if (e != hipSuccess) return fail(PAXISIM_EDEVICE, "linearizable: %s", hipGetErrorString(e));
-  if (anomalies) *anomalies = res[0];
-  if (ops) *ops = res[1];
-  if (skipped) *skipped = res[2];
+  h->lin_big = tot[LIN_BIG];
+  h->lin_nmax = tot[LIN_NMAX];
+  if (anomalies) *anomalies = res[LIN_ANOM];
+  if (ops) *ops = res[LIN_OPS];
+  if (skipped) *skipped = 0;   // no partition is too large (lin_big_kernel)
   return 0;
 }
 

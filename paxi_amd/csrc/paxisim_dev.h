@@ -78,6 +78,23 @@ __host__ __device__ inline uint32_t abd_ow(uint32_t outstanding) {
 constexpr uint32_t ABD_OPF = 6;   // op fields: tag, req, state|get<<2|set<<17, value, version, start
 enum { ABD_FREE = 0, ABD_GET = 1, ABD_SET = 2, ABD_DONE = 3 };
 
+// A scripted fault as the device reads it: the 40-byte paxisim_fault repacked
+// into three 16-byte-aligned words by paxisim_fault_add, so every load of the
+// table is a naturally aligned uint4 (the ABI struct is only 8-byte aligned).
+struct alignas(16) DevFault {
+  uint4 a;   // kind, src, dst, param
+  uint4 b;   // cluster_lo (lo, hi), cluster_hi (lo, hi)
+  uint4 c;   // step_from, step_to, 0, 0
+};
+__host__ inline DevFault dev_fault(const paxisim_fault& f) {
+  DevFault d;
+  d.a = make_uint4(f.kind, f.src, f.dst, f.param);
+  d.b = make_uint4((uint32_t)f.cluster_lo, (uint32_t)(f.cluster_lo >> 32), (uint32_t)f.cluster_hi,
+                   (uint32_t)(f.cluster_hi >> 32));
+  d.c = make_uint4(f.step_from, f.step_to, 0u, 0u);
+  return d;
+}
+
 struct Params {
   uint32_t protocol, N, Z, W, M, D, NS, WK, max_requests;
   uint32_t keys, write_ppm, locality_ppm, H, OW;
@@ -108,7 +125,7 @@ struct Params {
   uint32_t lds_bytes;      // LDS per cluster group (16-B multiple): the image + the stage
   uint32_t G;              // cluster groups (64-cluster tiles) per workgroup
   uint32_t rec_per_block;  // D*N*NS*M*64
-  const paxisim_fault* faults;
+  const DevFault* faults;
   // Paxos instance scalars [NI][C] (Multi-Paxos: NI = N); node scalars flags/nfwd [N][C]
   uint32_t *ballot, *slot, *execute, *meta, *flags, *npend, *nfwd;
   uint64_t* digest;
@@ -258,14 +275,13 @@ __device__ __forceinline__ bool scripted(const Params& P, uint32_t kind, uint64_
   for (uint32_t i = 0; i < P.nfaults; i++) {
     paxisim_fault f;
     {
-      const uint32_t* fw = reinterpret_cast<const uint32_t*>(&P.faults[i]);
-      const uint4 a = ldg(reinterpret_cast<const uint4*>(fw));
-      const uint4 b = ldg(reinterpret_cast<const uint4*>(fw + 4));
-      const uint32_t c0 = ldg(fw + 8), c1 = ldg(fw + 9);
+      const uint4 a = ldg(&P.faults[i].a);
+      const uint4 b = ldg(&P.faults[i].b);
+      const uint4 c = ldg(&P.faults[i].c);
       f.kind = a.x; f.src = a.y; f.dst = a.z; f.param = a.w;
       f.cluster_lo = (uint64_t)b.x | ((uint64_t)b.y << 32);
       f.cluster_hi = (uint64_t)b.z | ((uint64_t)b.w << 32);
-      f.step_from = c0; f.step_to = c1;
+      f.step_from = c.x; f.step_to = c.y;
     }
     if (f.kind != kind || f.src != src) continue;
     if (kind != PAXISIM_FAULT_CRASH && f.dst != PAXISIM_ALL_DST && f.dst != dst) continue;

@@ -349,8 +349,15 @@ __device__ __forceinline__ void handle_request(const Params& P, Rep<NT>& x, uint
 // the first replica to reach digest checkpoint k records it, every later one
 // compares (a 64-bit CAS, so concurrent arrivals in one step agree on who was
 // first; whether some pair disagrees does not depend on that order).
-static __device__ __noinline__ void agree_arrive(unsigned long long* a, uint32_t* st0, size_t sstride, uint32_t k,
-                                         uint64_t digest) {
+#ifndef PXS_AGREE_INLINE
+#define PXS_AGREE_INLINE 0
+#endif
+#if PXS_AGREE_INLINE
+__device__ __forceinline__
+#else
+static __device__ __noinline__
+#endif
+void agree_arrive(unsigned long long* a, uint32_t* st0, size_t sstride, uint32_t k, uint64_t digest) {
   const unsigned long long want = ((unsigned long long)k << 40) | ((digest ^ (digest >> 24)) & 0xFFFFFFFFFFull);
   unsigned long long v = atomicCAS(a, 0ull, want);
   uint32_t st = 0;                                       // 0: first to arrive, recorded

@@ -127,10 +127,9 @@ __device__ __forceinline__ ScriptedStep scripted_scan(const Params& P, const Rep
   ScriptedStep o = {0u, 0u, 0ull, false};
   const uint32_t N = nrep<NT>(P);
   for (uint32_t i = 0; i < P.nfaults; i++) {
-    const uint32_t* fw = reinterpret_cast<const uint32_t*>(&P.faults[i]);
-    const uint4 a = *reinterpret_cast<const uint4*>(fw);          // kind, src, dst, param
-    const uint4 b = *reinterpret_cast<const uint4*>(fw + 4);      // cluster_lo, cluster_hi
-    const uint2 c = *reinterpret_cast<const uint2*>(fw + 8);      // step_from, step_to
+    const uint4 a = P.faults[i].a;                                // kind, src, dst, param
+    const uint4 b = P.faults[i].b;                                // cluster_lo, cluster_hi
+    const uint4 c = P.faults[i].c;                                // step_from, step_to
     if (a.y != x.r) continue;
     const uint64_t lo = (uint64_t)b.x | ((uint64_t)b.y << 32), hi = (uint64_t)b.z | ((uint64_t)b.w << 32);
     if (x.gid < lo || x.gid >= hi || x.t < c.x || x.t >= c.y) continue;

@@ -258,7 +258,7 @@ def _zero(t, v):
     if v is None:
         return True
     if isinstance(t, int):
-        return t in (INT, UINT, BOOL) and v == 0 or t in (STRING, BYTES) and len(v) == 0
+        return t in (INT, UINT, BOOL, FLOAT, COMPLEX) and v == 0 or t in (STRING, BYTES) and len(v) == 0
     if isinstance(t, Slice):
         return len(v) == 0
     return False   # structs are always sent, an empty non-nil map too
@@ -274,6 +274,10 @@ def _enc_value(t, v, reg: TypeIds) -> bytes:
             return enc_bytes(v.encode() if isinstance(v, str) else v)
         if t == BYTES:
             return enc_bytes(v)
+        if t == FLOAT:
+            return enc_float(float(v))
+        if t == COMPLEX:                                   # real part, then imaginary
+            return enc_float(complex(v).real) + enc_float(complex(v).imag)
         if t == INTERFACE:
             raise GobError("only nil interface fields are encoded here")
         raise GobError(f"builtin {t} not supported")
@@ -459,6 +463,10 @@ class Decoder:
             return False
         if tid == STRING:
             return ""
+        if tid == FLOAT:                                  # Go's 0.0 and 0i for an omitted field
+            return 0.0
+        if tid == COMPLEX:
+            return 0j
         if tid == BYTES:
             return None
         if tid == INTERFACE:
@@ -545,7 +553,8 @@ def full(t, v):
     if isinstance(t, Slice):
         return [full(t.elem, e) for e in v or []]
     if v is None:
-        return 0 if t in (INT, UINT) else "" if t == STRING else False if t == BOOL else None
+        zero = {INT: 0, UINT: 0, STRING: "", BOOL: False, FLOAT: 0.0, COMPLEX: 0j}
+        return zero.get(t) if isinstance(t, int) else None
     if t == BYTES and len(v) == 0:
         return None
     return v

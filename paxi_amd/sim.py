@@ -48,6 +48,8 @@ def load_library():
     L.paxisim_occupancy.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     L.paxisim_active_clusters.restype = C.c_int
     L.paxisim_active_clusters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+    L.paxisim_read_activity.restype = C.c_int
+    L.paxisim_read_activity.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint32)]
     L.paxisim_device_bytes.restype = C.c_int
     L.paxisim_device_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     P = C.POINTER
@@ -76,7 +78,7 @@ EXPORTED = ["paxisim_abi_version", "paxisim_last_error", "paxisim_create", "paxi
             "paxisim_fault_add", "paxisim_step", "paxisim_sync", "paxisim_stats_get",
             "paxisim_read_state", "paxisim_read_instances", "paxisim_check", "paxisim_kernel_time", "paxisim_device_bytes",
             "paxisim_linearizable", "paxisim_history", "paxisim_occupancy", "paxisim_inject", "paxisim_read_log",
-            "paxisim_history_load", "paxisim_active_clusters", "paxisim_dist_init", "paxisim_dist_unique_id",
+            "paxisim_history_load", "paxisim_active_clusters", "paxisim_read_activity", "paxisim_dist_init", "paxisim_dist_unique_id",
             "paxisim_dist_init_rank", "paxisim_dist_allreduce", "paxisim_dist_stats", "paxisim_dist_destroy",
             "paxisim_read_kv", "paxisim_read_inbox", "paxisim_deliver", "paxisim_commands"]
 
@@ -212,6 +214,14 @@ class Simulation:
         b = C.c_uint64()
         _check(load_library().paxisim_active_clusters(self.h, C.byref(b)))
         return b.value
+
+    def activity(self, lo=0, n=None):
+        """Per cluster: None while the step kernels visit it, else the step at
+        which it froze at its fixed point (paxisim_read_activity)."""
+        n = self.cfg.clusters - lo if n is None else n
+        buf = (C.c_uint32 * max(1, n))()
+        _check(load_library().paxisim_read_activity(self.h, lo, n, buf))
+        return [None if buf[i] == 0xFFFFFFFF else buf[i] for i in range(n)]
 
     def device_bytes(self):
         b = C.c_uint64()

@@ -345,11 +345,13 @@ def capture(sim, cluster, steps):
 def export(sim, cluster, trace, outdir=None):
     """Per-link gob streams of a captured trace: {(src, dst): bytes} as a Paxi
     sender's encoder writes them, plus the schedule {"links": {"src->dst":
-    [steps]}, "client": [(step, dst, cid)]}.  One type-id registry plays the
-    exporting process.  With outdir, writes <src>-<dst>.gob files and
+    [steps]}, "client": [(step, dst, cid)]}.  Every sending replica is its own
+    Go process with its own type-id counter (encoding/gob's registry is per
+    process), so one registry per source replica is shared by that replica's
+    outgoing links.  With outdir, writes <src>-<dst>.gob files and
     schedule.json there."""
     codec = Codec(sim, cluster)
-    reg = gob.TypeIds()
+    regs = {}
     enc, sched, client = {}, {}, []
     N = trace["N"]
     for (t, src, dst, recs) in trace["msgs"]:
@@ -357,7 +359,9 @@ def export(sim, cluster, trace, outdir=None):
             client.append((t, dst, recs[0][4]))
             continue
         name, v = codec.to_go(src, recs)
-        e = enc.setdefault((src, dst), gob.Encoder(reg))
+        if (src, dst) not in enc:
+            enc[(src, dst)] = gob.Encoder(regs.setdefault(src, gob.TypeIds()))
+        e = enc[(src, dst)]
         e.encode_interface(name, v)
         sched.setdefault(f"{src}->{dst}", []).append(t)
     streams = {k: e.getvalue() for k, e in enc.items()}

@@ -45,6 +45,22 @@ kats = {
         {"name": "non_unique_value", "ops": [[1, None, 0, 5], [1, None, 0, 5], [None, 1, 6, 10], [None, 1, 6, 10]],
          "expect": 0},
     ],
+    # Tie order: Go's sort.Sort(byTime) is not stable, so ops
+    # with equal start have no defined order in the reference; here they keep
+    # the canonical order.  Five ops: W2 = write 2 [1,1], W1 = write 1 [2,2],
+    # Ra = read 0 [3,3], Rb = read 0 [4,4], R2 = read 2 [4,5]; orders a and b
+    # differ only in Rb / R2, which both start at 4.  Derived by hand from
+    # checker.go:69-104 with vertices in insertion order:
+    #   both: R2 merges into W2 (match), inheriting W1->W2 and Ra->W2; the DFS
+    #     from W2 finds W2->W1->W2 (gray {W2, W1}): anomaly 1; the cut removes
+    #     W1->W2 (start 2 > end 1), leaving the cycle W2->Ra->W2.
+    #   a: Rb was handled before R2 (no match, acyclic then) and no read
+    #     follows: 1 anomaly.
+    #   b: Rb comes after R2; Cycle() runs again and finds W2->W1->Ra->W2
+    #     (gray {W2, W1, Ra}): anomaly 2, cut Ra->W2 (3 > 1): 2 anomalies.
+    "lin_tie_order": {"a": [[2, None, 1, 1], [1, None, 2, 2], [None, 0, 3, 3], [None, 0, 4, 4], [None, 2, 4, 5]],
+                      "b": [[2, None, 1, 1], [1, None, 2, 2], [None, 0, 3, 3], [None, 2, 4, 5], [None, 0, 4, 4]],
+                      "expect_a": 1, "expect_b": 2},
     "config1": {
         "npz": [3], "writes": 1000, "target": 0,
         "delivered": {"P1a": 2, "P1b": 2, "P2a": 2000, "P2b": 2000, "P3": 2000},

@@ -222,6 +222,26 @@ def test_trace_stream_per_link_is_fifo():
         assert sched["links"][f"{src}->{dst}"] == sorted(sched["links"][f"{src}->{dst}"])
 
 
+def test_type_ids_are_per_sending_replica():
+    """Each replica is its own Go process: the first type a sender defines takes
+    id 65 in that sender's first stream, whatever other senders defined first."""
+    cfg, wl, fp = paxos_case()
+    a = OracleSim(cfg, wl, fp)
+    tr = trace.capture(a, 2, 60)
+    streams, _ = trace.export(a, 2, tr)
+    first_link = {}
+    for (t, s, d, recs) in tr["msgs"]:
+        if s < tr["N"]:
+            first_link.setdefault(s, (s, d))
+    assert len(first_link) >= 2
+    for src, link in first_link.items():
+        r = gob.Reader(streams[link])
+        m = gob.Reader(r.take(r.uint()))
+        assert m.int() == gob.INTERFACE and m.uint() == 0
+        m.take(m.uint())                                  # the registered name
+        assert m.int() == -65, f"sender {src}"
+
+
 def test_keyed_protocols_use_their_own_package():
     """m2paxos.Accept and wpaxos.Accept are distinct registered Go types: each
     protocol exports its own, and imports refuse the other's."""
@@ -323,3 +343,20 @@ def test_trace_cli_roundtrip_gpu(config, tmp_path):
     d = str(tmp_path)
     trace_cli.capture(argparse.Namespace(config=config, cluster=5, clusters=70, steps=150, crash_step=40, out=d))
     assert trace_cli.replay(argparse.Namespace(dir=d))
+
+
+def test_gob_omitted_float_and_complex_fields_decode_as_zero():
+    """Go omits zero-valued fields on the wire and decodes them as 0.0 and 0i."""
+    name = "example.Sample"
+    t = gob.Struct("Sample", [("X", gob.INT), ("F", gob.FLOAT), ("Z", gob.COMPLEX)])
+    gob.REGISTERED[name] = t
+    try:
+        e = gob.Encoder()
+        e.encode_interface(name, {"X": 3, "F": 0.0, "Z": 0j})
+        e.encode_interface(name, {"X": 0, "F": 17.0, "Z": complex(1.5, -2.0)})
+        got = list(gob.Decoder(e.getvalue()))
+        assert got == [(name, {"X": 3, "F": 0.0, "Z": 0j}), (name, {"X": 0, "F": 17.0, "Z": complex(1.5, -2.0)})]
+        assert isinstance(got[0][1]["F"], float) and isinstance(got[0][1]["Z"], complex)
+        assert gob.full(t, {"X": 3}) == {"X": 3, "F": 0.0, "Z": 0j}
+    finally:
+        del gob.REGISTERED[name]
