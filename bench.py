@@ -179,16 +179,23 @@ def host_physical_cores():
         return None
 
 
-def cpu_baseline(args, min_s=3.0):
+def cpu_baseline(args, sim=None, min_s=3.0):
     """The C oracle (same delivery schedule) over exactly the GPU leg's timed
     window of virtual steps, after the same warm-up: one thread on 256
     clusters, then all usable host threads on enough clusters for >= min_s
-    seconds (the rate changes along a run, so the window must match)."""
+    seconds (the rate changes along a run, so the window must match).
+
+    The oracle is the checker too: its samples end at the step the GPU handle
+    `sim` (rank 0: global clusters from 0) ended at, so the replica states of
+    those clusters must be equal; a second sample reruns random, WOVF- and
+    GHOST-flagged and frozen GPU clusters one by one (tests/parity_sample.py).
+    Both go into res["parity_sampled"]."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     threads, why = cpu_threads()
     warm, window = args.warmup * args.sim_steps, args.steps * args.sim_steps
     out = {}
+    checked = {"clusters": 0, "equal": 0}
 
     def sample(nthr, clusters):
         cfg, wl, fp, faults, _ = workload(args.config, clusters, 0, 0, args)
@@ -199,6 +206,14 @@ def cpu_baseline(args, min_s=3.0):
         o.step(window, threads=nthr)
         dt = time.perf_counter() - t0
         s1 = o.stats().as_dict()
+        if sim is not None:   # the checker: the same clusters on the GPU, at the same step
+            n = min(clusters, sim.cfg.clusters)
+            N = sim.N
+            a, b = sim.read_state(0, n), o.read_state(0, n)
+            eq = sum(1 for c in range(n) if all(a[c * N + r].as_tuple() == b[c * N + r].as_tuple()
+                                                for r in range(N)))
+            checked["clusters"] = max(checked["clusters"], n)
+            checked["equal"] = eq if n == checked["clusters"] else checked["equal"]
         o.close()
         return ((s1["delivered_total"] - s0["delivered_total"]) / dt, (s1["commits"] - s0["commits"]) / dt,
                 dt, clusters)
@@ -230,6 +245,18 @@ def cpu_baseline(args, min_s=3.0):
     if phys and phys > threads:
         # not measured: this process may use only `threads` CPUs of the host
         res["linear_estimate_all_physical_cores"] = v / threads * phys
+    if sim is not None:
+        import parity_sample
+        cfg, wl, fp, faults, _ = workload(args.config, sim.cfg.clusters, 0, 0, args)
+        picks = parity_sample.choose(sim, n_random=64, n_flag=32, n_frozen=32)
+        pr = parity_sample.check(sim, cfg, wl, fp, faults, warm + window, picks, threads=threads)
+        k = checked["clusters"] + pr["compared"]
+        eq = checked["equal"] + pr["equal"]
+        res["parity_sampled"] = f"{eq}/{k}"
+        res["parity_detail"] = {"contiguous_clusters": [0, checked["clusters"]], "contiguous_equal": checked["equal"],
+                                "picked": pr["by_kind"], "picked_equal": pr["equal"],
+                                "mismatches": pr["mismatches"], "at_step": warm + window,
+                                "compared": "every replica's paxisim_read_state record (+ instances / history)"}
     return res
 
 
@@ -249,6 +276,8 @@ def main():
     ap.add_argument("--kv", type=int, default=1, choices=[0, 1],
                     help="replicas execute into a Database (db.go Execute) - the reference always does")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-shard-check", action="store_true",
+                    help="skip the per-rank state digests (sharding invariance, SURVEY 8e)")
     args = ap.parse_args()
     for k, v in DEFAULTS[args.config].items():
         if getattr(args, k) is None:
@@ -316,6 +345,25 @@ def main():
         a, n, skipped = sim.linearizable()
         lin = {"anomalies": a, "ops_checked": n, "partitions_skipped": skipped, "scan_s": time.perf_counter() - tl}
 
+    # sharding invariance: every rank digests the states of its
+    # local clusters [C/2, C/2+256); at N=1 the same global ranges of ranks
+    # 1..7 are simulated by small handles of their own, so the N=8 run's rank-g
+    # digest must equal the N=1 run's "virtual" rank-g digest
+    shard_digests = None
+    if not args.no_shard_check:
+        dlo, dn = pdist.digest_range(args.clusters)
+        mine = pdist.state_digest(sim, dlo, dn)
+        got = pdist.gather_digests(mine, world)
+        if world == 1:
+            for g in range(1, 8):
+                c2, w2, f2, x2, _ = workload(args.config, dn, g * args.clusters + dlo, local, args)
+                s2 = Simulation(c2, w2, f2, x2)
+                s2.step((args.warmup + args.steps) * args.sim_steps)
+                got[g] = pdist.state_digest(s2, 0, dn)
+                s2.close()
+        shard_digests = {"clusters_per_rank": [dlo, dlo + dn], "digests": {str(k): v for k, v in got.items()},
+                         "virtual": world == 1}
+
     st1 = sim.stats()
     vals = pdist.stats_counters(d, alg_bytes(d), violations, s1["flagged"], agree_compared=st1.agree_compared,
                                 agree_missed=st1.agree_missed, active=sim.active_clusters())
@@ -382,8 +430,12 @@ def main():
             pass
         if lin is not None:
             out["linearizability"] = lin
+        if shard_digests is not None:
+            out["shard_digests"] = shard_digests
         if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args)
+            out["cpu_baseline"] = cpu_baseline(args, sim)
+            if "parity_sampled" in out["cpu_baseline"]:
+                out["parity_sampled"] = out["cpu_baseline"]["parity_sampled"]
         print(json.dumps(out), flush=True)
     if pd is not None:
         pd.close()

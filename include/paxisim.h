@@ -299,6 +299,19 @@ typedef struct paxisim_inbox_record {
   uint32_t cid;
 } paxisim_inbox_record;
 
+/* One closed-loop worker of a cluster (benchmark.go:246-275 worker): the
+ * command it waits on, how many it issued, and the Reply.Value of its last
+ * reply - Execute's return value, the key's value before the command
+ * (db.go:103-114, paxos.go:352-362; ABD: the value a read returned,
+ * abd/replica.go:145-150), as a command id (0 = nil; needs config.kv for the
+ * log-based protocols). */
+typedef struct paxisim_worker_state {
+  uint32_t cid;               /* current command id (0 = the worker is done) */
+  uint32_t issued;            /* requests issued */
+  uint32_t reply_value;       /* Reply.Value of the last reply */
+  uint32_t pad;
+} paxisim_worker_state;
+
 typedef struct paxisim paxisim;   /* opaque handle */
 
 int  paxisim_abi_version(void);
@@ -348,6 +361,10 @@ int  paxisim_commands(paxisim* h, uint64_t cluster, const uint32_t* cids, uint32
  * (mbox_cap records per link and step). */
 int  paxisim_deliver(paxisim* h, uint64_t cluster, uint32_t replica, uint32_t src,
                      const paxisim_inbox_record* recs, uint32_t n);
+
+/* The closed-loop workers of local cluster `cluster`: *n_out = outstanding
+ * records (cap of them written). */
+int  paxisim_read_client(paxisim* h, uint64_t cluster, paxisim_worker_state* out, uint32_t cap, uint32_t* n_out);
 
 /* Totals over the handle. */
 int  paxisim_stats_get(paxisim* h, paxisim_stats* out);
@@ -423,6 +440,12 @@ int  paxisim_active_clusters(paxisim* h, uint64_t* active);
  * of a cluster does not depend on it. */
 #define PAXISIM_STEPPED 0xFFFFFFFFu
 int  paxisim_read_activity(paxisim* h, uint64_t cluster_lo, uint64_t n, uint32_t* frozen_at);
+
+/* The quorum predicate the kernels evaluate (quorum.go:55-119 on an ack mask
+ * of replica indices in IDs.Less order), for the zones of cfg (n_zones, npz,
+ * fz): a host function, no device needed.  Lets a caller hold the kernels'
+ * predicates against its own quorum.go (sim.Quorum). */
+int  paxisim_quorum(const paxisim_config* cfg, uint32_t kind, uint32_t ack_mask, int* satisfied);
 
 /* Bytes of device memory held by the handle. */
 int  paxisim_device_bytes(paxisim* h, uint64_t* bytes);

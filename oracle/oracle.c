@@ -217,6 +217,7 @@ typedef struct replica {
   uint32_t delivered[PAXISIM_NMSG];
   uint32_t client_requests, sent, dropped, discarded, commits, replies;
   uint32_t agc, agm, agb;          /* agreement checkpoints compared / missed / mismatched */
+  uint32_t nag;                    /* agreement arrivals in the current step (AGMAX rule) */
   /* ABD (abd/replica.go:28-34): cid counter, versioned KV, op table */
   uint32_t abd_cid;
   uint32_t *kv_val, *kv_ver;
@@ -230,6 +231,7 @@ typedef struct cluster {
   uint32_t kc;
   uint32_t poison_step;            /* first step at which a replica panicked */
   uint32_t wk_cur[PAXISIM_MAX_WORKERS], wk_issued[PAXISIM_MAX_WORKERS];
+  uint32_t wk_rep[PAXISIM_MAX_WORKERS];   /* Reply.Value of the worker's last reply (0 = nil) */
   replica_t rep[PAXISIM_MAX_N];
   rec_t* mbox;                     /* [D][N][N+1][M] */
   uint64_t* agr;                   /* [NK][AR] first executor's digest per checkpoint: k << 40 | fold */
@@ -367,12 +369,14 @@ static void client_enqueue(ctx_t* x, uint32_t target, uint32_t cid) {
   (*cnt)++;
 }
 
-/* The HTTP response reaches worker w; it issues its next request. */
-static void client_reply(ctx_t* x, uint32_t cid) {
+/* The HTTP response reaches worker w (its Reply.Value kept: the value a
+ * read returned, benchmark.go:259-262); it issues its next request. */
+static void client_reply(ctx_t* x, uint32_t cid, uint32_t value) {
   const struct oracle_sim* s = x->s;
   uint32_t WK = s->wl.outstanding, w = (cid - 1u) % WK;
   if (x->c->wk_cur[w] != cid) return;                /* duplicate reply: worker moved on */
   x->n->replies++;
+  x->c->wk_rep[w] = value;
   if (s->wl.max_requests == 0 || x->c->wk_issued[w] < s->wl.max_requests) {
     uint64_t nc = 1ull + w + (uint64_t)WK * x->c->wk_issued[w];
     if (nc > CID_MAX) { raise_flag(x, PAXISIM_F_PEND_OVF | PAXISIM_F_UNFAITHFUL); x->c->wk_cur[w] = 0; return; }
@@ -386,10 +390,10 @@ static void client_reply(ctx_t* x, uint32_t cid) {
 
 /* Request.Reply (message.go:32-34): to the client, or back over the socket to
  * the node the request came from (node.go:83-90 reply goroutine). */
-static void request_reply(ctx_t* x, uint32_t req, uint32_t reply_cmd) {
+static void request_reply(ctx_t* x, uint32_t req, uint32_t reply_cmd, uint32_t value) {
   uint32_t o = REQ_ORIGIN(req);
-  if (o == PAXISIM_CLIENT_SRC) client_reply(x, REQ_CID(req));
-  else send1(x, o, PAXISIM_MSG_REPLY, 0, 0, reply_cmd);
+  if (o == PAXISIM_CLIENT_SRC) client_reply(x, REQ_CID(req), value);
+  else send1(x, o, PAXISIM_MSG_REPLY, value, 0, reply_cmd);   /* Reply{Command, Value}: value in the ballot word */
 }
 
 /* node.Forward (node.go:165-172): remember the request, send it to id. */
@@ -408,7 +412,7 @@ static void node_forward(ctx_t* x, uint32_t to, uint32_t req) {
 }
 
 /* node.recv Reply case (node.go:83-90): forwards[cmd].Reply(m). */
-static void handle_reply(ctx_t* x, uint32_t cid) {
+static void handle_reply(ctx_t* x, uint32_t cid, uint32_t value) {
   replica_t* p = x->n;
   uint32_t i;
   for (i = 0; i < p->nfwd; i++)
@@ -420,7 +424,7 @@ static void handle_reply(ctx_t* x, uint32_t cid) {
   {
     uint32_t req = p->fwd[i];
     p->fwd[i] = p->fwd[--p->nfwd];  /* retire (bounded memory) */
-    request_reply(x, req, cid);
+    request_reply(x, req, cid, value);
   }
 }
 
@@ -711,7 +715,7 @@ static void paxos_handle_p2b(ctx_t* x, uint32_t src, uint32_t mb, int32_t ms) { 
       broadcast1(x, PAXISIM_MSG_P3 | x->ktag, mb, (uint32_t)ms, e->cmd);
       if (x->s->cfg.reply_when_commit) {
         if (!e->req) { raise_flag(x, PAXISIM_F_POISON); x->stop = 1; return; } /* nil r.Reply */
-        request_reply(x, e->req, REQ_CID(e->req));         /* Reply{Command: r.Command} */
+        request_reply(x, e->req, REQ_CID(e->req), 0);      /* Reply{Command: r.Command}: no Value */
       } else {
         paxos_exec(x);
       }
@@ -737,7 +741,7 @@ static void paxos_handle_p3(ctx_t* x, uint32_t mb, int32_t ms, uint32_t mcid) { 
     e->cmd = mcid;
     e->meta |= E_COMMIT;
     if (x->s->cfg.reply_when_commit) {
-      if (e->req) request_reply(x, e->req, REQ_CID(e->req));
+      if (e->req) request_reply(x, e->req, REQ_CID(e->req), 0);
       return;
     }
   } else if (ms < p->execute) {
@@ -751,18 +755,33 @@ static void paxos_handle_p3(ctx_t* x, uint32_t mb, int32_t ms, uint32_t mcid) { 
 /* Agreement as a running check (client.go:279-320 Consensus: per index the
  * executed values form a set of size <= 1): the first replica to reach digest
  * checkpoint k (every CKI executed slots) records it in the cluster's ring,
- * every later one compares.  Which replica is first does not change whether
- * some pair disagrees, so this equals the device's concurrent version. */
+ * every later one compares.  Replicas run one after another within a step, so
+ * arrivals apply in replica index order, then arrival order - the order the
+ * device drains its per-step arrival lists in (sim_core.h agree_drain).  A
+ * replica's arrivals beyond AGMAX in one step count as missed (up to the
+ * device's 8-bit count of 255). */
+#define AGMAX 8
 static void agree_arrive(ctx_t* x, uint32_t k) {
   const uint32_t key = (uint32_t)(x->p - x->n->inst);
   uint64_t* a = &x->c->agr[(size_t)key * x->s->AR + k % x->s->AR];
   const uint64_t d = x->p->digest;
   const uint64_t want = ((uint64_t)k << 40) | ((d ^ (d >> 24)) & 0xFFFFFFFFFFull);
   const uint32_t tv = (uint32_t)(*a >> 40);
+  const uint32_t i = x->n->nag++;
+  if (i >= AGMAX) {
+    if (i < 255) x->n->agm++;
+    return;
+  }
   if (*a == 0 || tv < k) { *a = want; return; }
   if (tv > k) { x->n->agm++; return; }                      /* the first digest has left the ring */
   x->n->agc++;
   if (*a != want) x->n->agb++;
+}
+
+/* Database.Execute's return value (db.go:103-114): the key's value before the
+ * command (0 = nil), the Reply.Value of an executed request. */
+static uint32_t kv_get(ctx_t* x, uint32_t cmd) {
+  return x->s->kv ? x->n->db[wl_key(x->s, x->c->kc, cmd)] : 0u;
 }
 
 /* Database.Execute (db.go:103-114) when replicas keep the KV: a write's value
@@ -780,8 +799,8 @@ static void paxos_exec(ctx_t* x) {                         /* paxos.go:345-369 *
     entry_t* e = log_at(x, p->execute);
     if (!(e->meta & E_EXISTS) || !(e->meta & E_COMMIT)) break;
     if (x->p->iflags & PAXISIM_F_WOVF) raise_flag(x, PAXISIM_F_UNFAITHFUL);
-    if (e->req) {
-      request_reply(x, e->req, e->cmd);
+    if (e->req) {                                          /* Reply{Value: p.Execute(...)}: the previous value */
+      request_reply(x, e->req, e->cmd, kv_get(x, e->cmd));
       e->req = 0;
     }
     p->digest = mix64(p->digest ^ (((uint64_t)(uint32_t)p->execute << 32) | e->cmd));
@@ -810,7 +829,7 @@ static void paxos_dispatch(ctx_t* x, uint32_t src, const rec_t* m) {
     case PAXISIM_MSG_REQUEST:
       replica_handle_request(x, REQ(m->cid, src == x->s->N ? PAXISIM_CLIENT_SRC : src));
       break;
-    case PAXISIM_MSG_REPLY: handle_reply(x, m->cid); break;
+    case PAXISIM_MSG_REPLY: handle_reply(x, m->cid, m->ballot); break;
     case PAXISIM_MSG_P1A: paxos_handle_p1a(x, m->ballot); break;
     case PAXISIM_MSG_P1B: paxos_handle_p1b(x, src, m->ballot, m + 1, HDR_N(m->hdr)); break;
     case PAXISIM_MSG_P2A: paxos_handle_p2a(x, m->ballot, (int32_t)m->slot, m->cid); break;
@@ -993,7 +1012,7 @@ static void wpaxos_dispatch(ctx_t* x, uint32_t src, const rec_t* m) {   /* regis
     case PAXISIM_MSG_REQUEST:
       wp_handle_request(x, REQ(m->cid, src == x->s->N ? PAXISIM_CLIENT_SRC : src));
       break;
-    case PAXISIM_MSG_REPLY: handle_reply(x, m->cid); break;
+    case PAXISIM_MSG_REPLY: handle_reply(x, m->cid, m->ballot); break;
     case PAXISIM_MSG_P1A: wp_init(x, key); paxos_handle_p1a(x, m->ballot); break;          /* handlePrepare 72-76 */
     case PAXISIM_MSG_P1B:                                                                  /* handlePromise 78-82 */
       if (wp_get(x, key)) paxos_handle_p1b(x, src, m->ballot, m + 1, HDR_N(m->hdr));
@@ -1093,11 +1112,11 @@ static void ep_broadcast(ctx_t* x, uint32_t type, uint32_t w1, uint32_t w2, uint
     if (d != x->r) ep_send(x, d, type, w1, w2, w3, pay, npay);
 }
 
-static void ep_reply(ctx_t* x, ep_inst_t* i) {           /* i.request.Reply (message.go:32-34) */
+static void ep_reply(ctx_t* x, ep_inst_t* i, uint32_t value) { /* i.request.Reply (message.go:32-34) */
   /* req.c is buffered 1 (http.go:97): the HTTP handler takes the first reply,
    * the second waits in the buffer, a third would block this goroutine */
   if (++i->nrep >= 3) raise_flag(x, PAXISIM_F_UNFAITHFUL);
-  request_reply(x, i->req, i->cmd);
+  request_reply(x, i->req, i->cmd, value);
 }
 
 /* execute (replica.go:355-384): owners in index order where Go ranges over a map */
@@ -1115,7 +1134,11 @@ static void ep_execute(ctx_t* x) {
       if (i->status != EP_COMMITTED) break;
       p->inst[0].digest = mix64(p->inst[0].digest ^ (((uint64_t)((id << 24) | (uint32_t)sl) << 32) | i->cmd));
       p->ep_execs++;
-      kv_exec(x, i->cmd);
+      {
+        const uint32_t v = kv_get(x, i->cmd);               /* v := r.Execute(i.cmd), replica.go:373 */
+        kv_exec(x, i->cmd);
+        if (i->req) ep_reply(x, i, v);
+      }
       if (s->keep_xlog) {
         inst_t* q = &p->inst[0];
         if (q->nx == q->capx) {
@@ -1124,7 +1147,6 @@ static void ep_execute(ctx_t* x) {
         }
         q->xlog[q->nx++] = i->cmd;
       }
-      if (i->req) ep_reply(x, i);
       if (sl == p->ep_executed[id] + 1) {
         const uint32_t k = ep_key(x, i->cmd);
         int32_t* cf = ep_cf(x, id, k);
@@ -1235,7 +1257,7 @@ static void ep_handle_preaccept_reply(ctx_t* x, uint32_t src, const rec_t* m) { 
       p->commits++;
       ep_update_commit(x, x->r);
       ep_commit_broadcast(x, i, sl);
-      if (s->cfg.reply_when_commit && i->req) ep_reply(x, i);
+      if (s->cfg.reply_when_commit && i->req) ep_reply(x, i, 0);
     } else {                                               /* slow path */
       uint32_t pay[PAXISIM_MAX_N], k;
       i->status = EP_ACCEPTED;
@@ -1276,7 +1298,7 @@ static void ep_handle_accept_reply(ctx_t* x, uint32_t src, const rec_t* m) {   /
     i->status = EP_COMMITTED;
     x->n->commits++;
     ep_update_commit(x, x->r);
-    if (x->s->cfg.reply_when_commit && i->req) ep_reply(x, i);
+    if (x->s->cfg.reply_when_commit && i->req) ep_reply(x, i, 0);
     ep_commit_broadcast(x, i, sl);
   }
 }
@@ -1315,7 +1337,7 @@ static void epaxos_dispatch(ctx_t* x, uint32_t src, const rec_t* m) {   /* regis
     case PAXISIM_MSG_REQUEST:
       ep_handle_request(x, REQ(m->cid, src == x->s->N ? PAXISIM_CLIENT_SRC : src));
       break;
-    case PAXISIM_MSG_REPLY: handle_reply(x, m->cid); break;
+    case PAXISIM_MSG_REPLY: handle_reply(x, m->cid, m->ballot); break;
     case PAXISIM_MSG_PREACCEPT: ep_handle_preaccept(x, src, m); break;
     case PAXISIM_MSG_PREACCEPTREPLY: ep_handle_preaccept_reply(x, src, m); break;
     case PAXISIM_MSG_ACCEPT: ep_handle_accept(x, src, m); break;
@@ -1428,7 +1450,7 @@ static void abd_handle_setreply(ctx_t* x, uint32_t src, uint32_t key, uint32_t o
     } else if (x->s->cfg.history) {
       raise_flag(x, PAXISIM_F_HIST_OVF);
     }
-    client_reply(x, e->req);
+    client_reply(x, e->req, w ? 0u : e->value);          /* Reply{Value: e.value} for a read only */
   }
 }
 
@@ -1496,6 +1518,7 @@ static void replica_step(const struct oracle_sim* s, cluster_t* c, uint32_t r, u
   x.r = r; x.t = t; x.stop = 0;
   x.hs = step_key(c->kc, t);
   x.n->send_seq = 0;
+  x.n->nag = 0;
   if (s->late_workers) client_start(&x);
   fault_process(&x);
   crash = crashed(s, c, r, t);
@@ -2288,6 +2311,20 @@ int oracle_read_kv(oracle_sim* s, uint64_t cl, uint32_t r, uint32_t* out, uint32
     else if (s->kv) out[k] = p->db[k];
     else return fail(PAXISIM_EUNSUPP, "replicas keep no Database (config.kv = 0)");
   }
+  return 0;
+}
+
+int oracle_read_client(oracle_sim* s, uint64_t cl, paxisim_worker_state* out, uint32_t cap, uint32_t* n_out) {
+  uint32_t w, n;
+  if (!s || !n_out || cl >= s->C || (cap && !out)) return fail(PAXISIM_EINVAL, "bad argument");
+  n = s->wl.outstanding;
+  for (w = 0; w < n && w < cap; w++) {
+    out[w].cid = s->cl[cl].wk_cur[w];
+    out[w].issued = s->cl[cl].wk_issued[w];
+    out[w].reply_value = s->cl[cl].wk_rep[w];
+    out[w].pad = 0;
+  }
+  *n_out = n;
   return 0;
 }
 

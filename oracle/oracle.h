@@ -47,6 +47,7 @@ int  oracle_exec_log(oracle_sim* h, uint64_t cluster, uint32_t replica,
 int  oracle_lin_check(oracle_sim* h, uint64_t* anomalies, uint64_t* ops);
 int  oracle_history(oracle_sim* h, uint64_t cluster, uint32_t* buf, uint32_t cap_ops, uint32_t* n_out);
 int  oracle_read_kv(oracle_sim* h, uint64_t cluster, uint32_t replica, uint32_t* values, uint32_t n);
+int  oracle_read_client(oracle_sim* h, uint64_t cluster, paxisim_worker_state* out, uint32_t cap, uint32_t* n_out);
 int  oracle_command(oracle_sim* h, uint64_t cluster, uint32_t cid, uint32_t* key, uint32_t* write);
 int  oracle_history_load(oracle_sim* h, uint64_t cluster, uint32_t replica, const uint32_t* ops, uint32_t n);
 const char* oracle_last_error(void);

@@ -174,6 +174,14 @@ class InboxRecord(C.Structure):
         return (self.src, self.hdr, self.ballot, self.slot, self.cid)
 
 
+class WorkerState(C.Structure):
+    """paxisim_worker_state: a closed-loop worker (benchmark.go:246-275) and its last Reply.Value."""
+    _fields_ = [("cid", C.c_uint32), ("issued", C.c_uint32), ("reply_value", C.c_uint32), ("pad", C.c_uint32)]
+
+    def as_tuple(self):
+        return (self.cid, self.issued, self.reply_value)
+
+
 class Stats(C.Structure):
     _fields_ = [
         ("steps", C.c_uint64), ("clusters", C.c_uint64),

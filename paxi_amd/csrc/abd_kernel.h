@@ -119,8 +119,8 @@ __device__ __forceinline__ void abd_handle_setreply(const Params& P, Rep<NT>& x,
     sm = (sm & ~3u) | ABD_DONE;
     x.commits++;
     const uint32_t req = x.l_c[op_i<NT>(P, x, opid, 1)];
+    const uint32_t w = wl_write(P, x.kc, req) ? 1u : 0u;
     if ((uint32_t)x.execute < P.H) {                   // History.AddOperation (history.go:44-52)
-      const uint32_t w = wl_write(P, x.kc, req) ? 1u : 0u;
       P.hist[((size_t)x.r * P.C + x.c) * P.H + (uint32_t)x.execute] =
           make_uint4(key | (w << 31), x.l_c[op_i<NT>(P, x, opid, 3)], x.l_c[op_i<NT>(P, x, opid, 5)], x.t);
       x.execute++;
@@ -128,7 +128,7 @@ __device__ __forceinline__ void abd_handle_setreply(const Params& P, Rep<NT>& x,
       x.flags |= PAXISIM_F_HIST_OVF;
     }
     x.l_c[si] = sm;
-    client_reply<NT>(P, x, req);
+    client_reply<NT>(P, x, req, w ? 0u : x.l_c[op_i<NT>(P, x, opid, 3)]);   // Reply{Value: e.value} for a read
     return;
   }
   x.l_c[si] = sm;

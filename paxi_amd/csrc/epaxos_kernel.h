@@ -167,9 +167,9 @@ __device__ __forceinline__ void ep_broadcast(const Params& P, Rep<NT>& x, uint32
 // i.request.Reply (message.go:32-34): req.c is buffered 1 (http.go:97), so the
 // HTTP handler takes the first reply, the second waits, a third would block
 template <int NT>
-__device__ __forceinline__ void ep_reply(const Params& P, Rep<NT>& x, EpI& e) {
+__device__ __forceinline__ void ep_reply(const Params& P, Rep<NT>& x, EpI& e, uint32_t value) {
   if (++e.nrep >= 3u) x.flags |= PAXISIM_F_UNFAITHFUL;
-  request_reply<NT>(P, x, e.req, e.cmd);
+  request_reply<NT>(P, x, e.req, e.cmd, value);
 }
 
 // execute (replica.go:355-384): owners in index order where Go ranges over a map
@@ -188,9 +188,10 @@ __device__ void ep_execute(const Params& P, Rep<NT>& x) {
       if (e.status != EP_COMMITTED) break;
       x.digest = mix64(x.digest ^ (((uint64_t)((id << 24) | (uint32_t)sl) << 32) | e.cmd));
       x.execute++;                                       // Execute calls, re-executions included
+      const uint32_t v = P.kv && e.req ? kv_get<NT>(P, x, e.cmd) : 0u;   // v := r.Execute(i.cmd)
       if (P.kv) kv_exec<NT>(P, x, e.cmd);
       if (e.req) {
-        ep_reply<NT>(P, x, e);
+        ep_reply<NT>(P, x, e, v);
         P.ep_inst[ii] = make_uint4(e.cmd, e.req, e.acks | (e.nrep << 16), (uint32_t)e.seq);
       }
       if (sl == ep_get<NT>(P, x, 2, id) + 1) {
@@ -343,7 +344,7 @@ __device__ void ep_handle_preaccept_reply(const Params& P, Rep<NT>& x, uint32_t 
       ep_load<NT>(P, x, ii, e);                          // execute() may have replied
       ep_commit_broadcast<NT>(P, x, e, sl);
       if (P.rwc && e.req) {
-        ep_reply<NT>(P, x, e);
+        ep_reply<NT>(P, x, e, 0u);
         ep_store<NT>(P, ii, e);
       }
       return;
@@ -414,7 +415,7 @@ __device__ void ep_handle_accept_reply(const Params& P, Rep<NT>& x, uint32_t src
     ep_update_commit<NT>(P, x, x.r);
     ep_load<NT>(P, x, ii, e);
     if (P.rwc && e.req) {
-      ep_reply<NT>(P, x, e);
+      ep_reply<NT>(P, x, e, 0u);
       ep_store<NT>(P, ii, e);
     }
     ep_commit_broadcast<NT>(P, x, e, sl);
@@ -512,7 +513,7 @@ struct EPaxosProto {
                                                   uint32_t ri) {
     switch (hdr_type(m.x)) {
       case PAXISIM_MSG_REQUEST: dv_inc<NT>(x, PAXISIM_MSG_REQUEST); ep_handle_request<NT>(P, x, mkreq(m.w, src)); break;
-      case PAXISIM_MSG_REPLY: dv_inc<NT>(x, PAXISIM_MSG_REPLY); handle_reply<NT>(P, x, m.w); break;
+      case PAXISIM_MSG_REPLY: dv_inc<NT>(x, PAXISIM_MSG_REPLY); handle_reply<NT>(P, x, m.w, m.y); break;
       case PAXISIM_MSG_PREACCEPT: dv_inc<NT>(x, PAXISIM_MSG_PREACCEPT); ep_handle_preaccept<NT>(P, x, src, m, ri); break;
       case PAXISIM_MSG_PREACCEPTREPLY:
         dv_inc<NT>(x, PAXISIM_MSG_PREACCEPTREPLY);

@@ -505,6 +505,7 @@ __device__ void swap_slots(const Params& P, uint64_t p, uint64_t q, uint32_t j) 
   swap_rows(P.agr, (size_t)P.AR * P.NK, C, p, q, j);
   swap_rows(P.kv_val, P.kv ? (size_t)P.keys * N : 0, C, p, q, j);
   swap_rows(P.kv_ver, P.kv ? N : 0, C, p, q, j);
+  swap_rows(P.wrep, P.WK, C, p, q, j);
   swap_rows(P.frz, 1, C, p, q, j);
   swap_rows(P.qf, 1, C, p, q, j);
   swap_lanes(P.reqx, (size_t)N * P.W * LANES, (size_t)N * P.W, p, q, j);
@@ -871,19 +872,24 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     if (maxthr <= 0) maxthr = (int)(N * LANES);
     const uint32_t alloc = ((uint32_t)vgprs + 7u) / 8u * 8u;
     const uint32_t wps = alloc >= 512u ? 1u : (512u / alloc < 8u ? 512u / alloc : 8u);
+    // per tile: the image, the agreement-ring arrival counts (not persisted:
+    // drained every step), then the stage
+    const uint32_t agn = P.AR ? (2u * N * LANES + 15u) & ~15u : 0u;
+    const uint32_t base = P.img.bytes + agn;
     uint32_t G = 1, gmax = 4;
     if (const char* e = getenv("PAXISIM_GROUPS")) gmax = (uint32_t)atoi(e) ? (uint32_t)atoi(e) : 1u;   // tuning
     for (uint32_t g = 2; g <= gmax; g++)
-      if ((g * N + 3u) / 4u <= wps && g * N * LANES <= (uint32_t)maxthr && g * P.img.bytes <= LDS_MAX) G = g;
+      if ((g * N + 3u) / 4u <= wps && g * N * LANES <= (uint32_t)maxthr && g * base <= LDS_MAX) G = g;
     P.G = G;
     // LDS stage for the first J picks of every replica's step, from what the groups leave
     uint32_t jmax = 16;
     if (const char* e = getenv("PAXISIM_STAGE")) jmax = (uint32_t)atoi(e);   // tuning override
-    const uint32_t room = (LDS_MAX / G - P.img.bytes) / (N * LANES * 16u);
+    const uint32_t room = (LDS_MAX / G - base) / (N * LANES * 16u);
     P.J = room < jmax ? room : jmax;
     if (!h->ops.staged) P.J = 0;   // that instance has no staged loop
-    P.off_stage = P.img.bytes;
-    P.lds_bytes = P.img.bytes + P.J * N * LANES * 16u;
+    P.off_agn = P.img.bytes;
+    P.off_stage = base;
+    P.lds_bytes = base + P.J * N * LANES * 16u;
   }
   P.C = (cfg->clusters + LANES * P.G - 1) / (LANES * P.G) * (LANES * P.G);
   const size_t C = P.C, NC = (size_t)N * C, NIC = (size_t)P.NI * C, blocks = C / LANES;
@@ -910,6 +916,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     uint4* hist = carve<uint4>(p, NC * P.H);
     uint32_t* maps = carve<uint32_t>(p, C * 4);
     unsigned long long* agr = carve<unsigned long long>(p, (size_t)P.AR * P.NK * C);
+    uint4* agq = carve<uint4>(p, P.AR ? (size_t)2 * AGMAX * N * C : 0);
     const bool ep = P.protocol == PAXISIM_EPAXOS;
     uint4* ep_inst = carve<uint4>(p, ep ? (size_t)N * N * P.W * C * 4 : 0);
     uint32_t* ep_sce = carve<uint32_t>(p, ep ? (size_t)3 * N * N * C : 0);
@@ -917,6 +924,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     uint32_t* ep_max = carve<uint32_t>(p, ep ? (size_t)P.keys * N * C : 0);
     uint32_t* kv_val = carve<uint32_t>(p, P.kv ? (size_t)P.keys * N * C : 0);
     uint32_t* kv_ver = carve<uint32_t>(p, P.kv ? (size_t)N * C : 0);
+    uint32_t* wrep = carve<uint32_t>(p, (size_t)P.WK * C);
     uint8_t* image = carve<uint8_t>(p, blocks * P.img.bytes);
     char* zend = p;
     uint4* rec = carve<uint4>(p, blocks * P.rec_per_block);
@@ -929,8 +937,9 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
       P.wst = wst; P.wlog = wlog; P.wpend = wpend; P.gst = gst; P.wpx = wpx;
       P.slot_of = maps; P.cl_of = maps + C; P.frz = maps + 2 * C; P.qf = maps + 3 * C;
       P.agr = agr;
+      P.agq = agq;
       P.ep_inst = ep_inst; P.ep_sce = ep_sce; P.ep_cf = ep_cf; P.ep_max = ep_max;
-      P.kv_val = kv_val; P.kv_ver = kv_ver;
+      P.kv_val = kv_val; P.kv_ver = kv_ver; P.wrep = wrep;
     }
     return std::make_pair((size_t)zend, (size_t)p);
   };
@@ -1044,6 +1053,41 @@ static int wake(paxisim* h, uint64_t cluster) {
   return 0;
 }
 
+__global__ void read_client_kernel(Params P, uint64_t cl, paxisim_worker_state* out) {
+  const uint32_t w = threadIdx.x;
+  if (w >= P.WK) return;
+  const uint64_t c = slot_of(P, cl);
+  const uint8_t* img = P.image + (c / LANES) * (size_t)P.img.bytes;
+  const uint32_t wi = (w << 6) | (uint32_t)(c % LANES);
+  paxisim_worker_state s;
+  s.cid = reinterpret_cast<const uint32_t*>(img + P.img.off_wcur)[wi];
+  s.issued = reinterpret_cast<const uint32_t*>(img + P.img.off_wiss)[wi];
+  s.reply_value = P.wrep[(size_t)w * P.C + c];
+  s.pad = 0;
+  out[w] = s;
+}
+
+extern "C" int paxisim_read_client(paxisim* h, uint64_t cluster, paxisim_worker_state* out, uint32_t cap,
+                                   uint32_t* n_out) {
+  if (!h || !n_out || (cap && !out)) return fail(PAXISIM_EINVAL, "null argument");
+  if (cluster >= h->cfg.clusters) return fail(PAXISIM_ERANGE, "bad cluster");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const uint32_t n = h->P.WK;
+  *n_out = n;
+  if (!cap || !n) return 0;
+  paxisim_worker_state* d = nullptr;
+  HIPCHK(hipMalloc(&d, n * sizeof(paxisim_worker_state)));
+  read_client_kernel<<<1, 64, 0, h->stream>>>(h->P, cluster, d);
+  hipError_t e = hipGetLastError();
+  std::vector<paxisim_worker_state> tmp(n);
+  if (e == hipSuccess) e = hipMemcpyAsync(tmp.data(), d, n * sizeof(paxisim_worker_state), hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(PAXISIM_EDEVICE, "read_client: %s", hipGetErrorString(e));
+  for (uint32_t w = 0; w < n && w < cap; w++) out[w] = tmp[w];
+  return 0;
+}
+
 __global__ void read_kv_kernel(Params P, uint64_t cl, uint32_t r, uint32_t n, uint32_t* out) {
   const uint32_t k = threadIdx.x + blockIdx.x * blockDim.x;
   if (k >= n) return;
@@ -1089,6 +1133,21 @@ __global__ void activity_kernel(Params P, uint64_t lo, uint64_t n, uint32_t* out
   if (i >= n) return;
   const uint64_t s = slot_of(P, lo + i);
   out[i] = s < *P.bound ? 0xFFFFFFFFu : P.frz[s];
+}
+
+extern "C" int paxisim_quorum(const paxisim_config* cfg, uint32_t kind, uint32_t ack_mask, int* satisfied) {
+  if (!cfg || !satisfied) return fail(PAXISIM_EINVAL, "null argument");
+  if (cfg->n_zones == 0 || cfg->n_zones > PAXISIM_MAX_ZONES || kind > PAXISIM_Q_FGRID_Q2)
+    return fail(PAXISIM_EINVAL, "bad zones or quorum kind");
+  uint32_t npz[PAXISIM_MAX_ZONES], zmask[PAXISIM_MAX_ZONES], N = 0;
+  for (uint32_t z = 0; z < cfg->n_zones; z++) {
+    if (cfg->npz[z] == 0 || N + cfg->npz[z] > PAXISIM_MAX_N) return fail(PAXISIM_EINVAL, "bad nodes per zone");
+    npz[z] = cfg->npz[z];
+    zmask[z] = ((1u << npz[z]) - 1u) << N;
+    N += npz[z];
+  }
+  *satisfied = quorum_check(kind, N, cfg->n_zones, npz, zmask, cfg->fz, ack_mask & ((1u << N) - 1u)) ? 1 : 0;
+  return 0;
 }
 
 extern "C" int paxisim_read_activity(paxisim* h, uint64_t lo, uint64_t n, uint32_t* frozen_at) {

@@ -24,6 +24,7 @@ constexpr uint32_t FMAX = 32;   // forwards table per replica (node.forwards)
 constexpr uint32_t CKI = 16;    // checkpoint interval (executed slots)
 constexpr uint32_t CKR = 8;     // checkpoints kept per replica
 constexpr uint32_t GMAX = 8;    // live entries below execute kept per instance
+constexpr uint32_t AGMAX = 8;   // agreement-ring arrivals buffered per replica-step
 constexpr uint32_t NO_ID = 0xFFu;
 constexpr uint32_t POL_NONE = 0xFFu;   // consecutive.last == "" (policy.go:50)
 constexpr uint32_t LANES = 64;
@@ -146,6 +147,8 @@ struct Params {
   uint32_t* stats;       // [NSTAT][N][C]
   unsigned long long* agr;  // [AR][NK][C] first executor's digest per checkpoint: k << 40 | 40-bit digest fold
   uint32_t AR;           // checkpoints kept per (cluster, instance); 0 = no agreement ring
+  uint4* agq;            // [2][AGMAX][N][C] a step's ring arrivals {entry lo, entry hi, key, 0}, by step parity
+  uint32_t off_agn;      // LDS byte offset of the arrival counts [2][N][lane] u8 (per tile, outside the image)
   uint32_t* reqx;        // [blk][N][W][64] request side table (Paxos)
   uint4* hist;           // [N][C][H] completed ABD ops {key|write<<31, value, start, end}
   uint8_t* image;        // [blk][img.bytes]
@@ -174,6 +177,7 @@ struct Params {
   uint32_t kv;
   uint32_t* kv_val;      // [K][r][C] value = command id of the last write, 0 = nil
   uint32_t* kv_ver;      // [r][C] database.version
+  uint32_t* wrep;        // [WK][C] Reply.Value of each worker's last reply (0 = nil)
 };
 
 // slot of local cluster c
@@ -223,27 +227,33 @@ __device__ __forceinline__ uint32_t rec_len(uint32_t h) {
 }
 
 // ---- quorum predicates on an ack mask (quorum.go:55-119) -----------------
-__device__ __forceinline__ bool quorum_ok(const Params& P, uint32_t kind, uint32_t mask) {
-  const int size = __popc(mask);
-  if (kind == PAXISIM_Q_MAJORITY) return size > (int)(P.N / 2);
+// One definition for the kernels and the host (paxisim_quorum exports it, so
+// a caller can check the predicates the kernels use against quorum.go).
+__host__ __device__ __forceinline__ bool quorum_check(uint32_t kind, uint32_t N, uint32_t Z, const uint32_t* npz,
+                                                      const uint32_t* zmask, uint32_t fz, uint32_t mask) {
+  const int size = __builtin_popcount(mask);
+  if (kind == PAXISIM_Q_MAJORITY) return size > (int)(N / 2);
   uint32_t zones_any = 0, zones_maj = 0;
   bool col = false;
-  for (uint32_t z = 0; z < P.Z; z++) {
-    const uint32_t c = (uint32_t)__popc(mask & P.zmask[z]);
+  for (uint32_t z = 0; z < Z; z++) {
+    const uint32_t c = (uint32_t)__builtin_popcount(mask & zmask[z]);
     zones_any += c > 0;
-    zones_maj += c > P.npz[z] / 2;
-    col |= c == P.npz[z];
+    zones_maj += c > npz[z] / 2;
+    col |= c == npz[z];
   }
   switch (kind) {
-    case PAXISIM_Q_ALL: return size == (int)P.N;
-    case PAXISIM_Q_FAST: return size >= (int)(P.N * 3 / 4);
-    case PAXISIM_Q_GRID_ROW: return zones_any == P.Z;
+    case PAXISIM_Q_ALL: return size == (int)N;
+    case PAXISIM_Q_FAST: return size >= (int)(N * 3 / 4);
+    case PAXISIM_Q_GRID_ROW: return zones_any == Z;
     case PAXISIM_Q_ZONE_MAJORITY: return zones_maj > 0;
     case PAXISIM_Q_GRID_COLUMN: return col;
-    case PAXISIM_Q_FGRID_Q1: return (int)zones_maj >= (int)P.Z - (int)P.fz;
-    case PAXISIM_Q_FGRID_Q2: return (int)zones_maj >= (int)P.fz + 1;
+    case PAXISIM_Q_FGRID_Q1: return (int)zones_maj >= (int)Z - (int)fz;
+    case PAXISIM_Q_FGRID_Q2: return (int)zones_maj >= (int)fz + 1;
   }
   return false;
+}
+__device__ __forceinline__ bool quorum_ok(const Params& P, uint32_t kind, uint32_t mask) {
+  return quorum_check(kind, P.N, P.Z, P.npz, P.zmask, P.fz, mask);
 }
 
 // ---- loads retired on the spot ----------------------------------------------

@@ -131,11 +131,13 @@ __device__ __forceinline__ uint32_t eset_cmd(const Params& P, Rep<NT>& x, uint32
 // ---------------------------------------------------------------------------
 // Request.Reply routing (node.go:83-97) and node.Forward (node.go:165-172)
 // ---------------------------------------------------------------------------
+// The Reply's Value (0 = nil) rides in the record's ballot word.
 template <int NT>
-__device__ __forceinline__ void request_reply(const Params& P, Rep<NT>& x, uint32_t req, uint32_t reply_cmd) {
+__device__ __forceinline__ void request_reply(const Params& P, Rep<NT>& x, uint32_t req, uint32_t reply_cmd,
+                                              uint32_t value) {
   const uint32_t o = req_origin(req);
-  if (o == PAXISIM_CLIENT_SRC) client_reply<NT>(P, x, req_cid(req));
-  else post_unicast<NT>(P, x, o, PAXISIM_MSG_REPLY, 0u, 0u, reply_cmd);
+  if (o == PAXISIM_CLIENT_SRC) client_reply<NT>(P, x, req_cid(req), value);
+  else post_unicast<NT>(P, x, o, PAXISIM_MSG_REPLY, value, 0u, reply_cmd);
 }
 
 // node.Forward (node.go:165-172)
@@ -174,7 +176,7 @@ __device__ __forceinline__ void node_forward(const Params& P, Rep<NT>& x, uint32
 
 // node.recv Reply case (node.go:83-90)
 template <int NT>
-__device__ __forceinline__ void handle_reply(const Params& P, Rep<NT>& x, uint32_t cid) {
+__device__ __forceinline__ void handle_reply(const Params& P, Rep<NT>& x, uint32_t cid, uint32_t value) {
   const uint32_t i = fwd_find<NT>(P, x, cid);
   if (i == x.nfwd) {
     x.flags |= PAXISIM_F_UNFAITHFUL;
@@ -183,7 +185,7 @@ __device__ __forceinline__ void handle_reply(const Params& P, Rep<NT>& x, uint32
   const uint32_t req = ldg(&P.fwd[krc(P, i, x.r, x.c)]);
   x.nfwd--;
   P.fwd[krc(P, i, x.r, x.c)] = ldg(&P.fwd[krc(P, x.nfwd, x.r, x.c)]);
-  request_reply<NT>(P, x, req, cid);
+  request_reply<NT>(P, x, req, cid, value);
 }
 
 // ---------------------------------------------------------------------------
@@ -345,38 +347,16 @@ __device__ __forceinline__ void handle_request(const Params& P, Rep<NT>& x, uint
   else node_forward<NT>(P, x, bal_id(x.ballot), req);
 }
 
-// Agreement ring (client.go:279-320 Consensus, restated as a running check):
-// the first replica to reach digest checkpoint k records it, every later one
-// compares (a 64-bit CAS, so concurrent arrivals in one step agree on who was
-// first; whether some pair disagrees does not depend on that order).
-#ifndef PXS_AGREE_INLINE
-#define PXS_AGREE_INLINE 0
-#endif
-#if PXS_AGREE_INLINE
-__device__ __forceinline__
-#else
-static __device__ __noinline__
-#endif
-void agree_arrive(unsigned long long* a, uint32_t* st0, size_t sstride, uint32_t k, uint64_t digest) {
-  const unsigned long long want = ((unsigned long long)k << 40) | ((digest ^ (digest >> 24)) & 0xFFFFFFFFFFull);
-  unsigned long long v = atomicCAS(a, 0ull, want);
-  uint32_t st = 0;                                       // 0: first to arrive, recorded
-  while (v != 0ull) {
-    const uint32_t tv = (uint32_t)(v >> 40);
-    if (tv == k) { st = v == want ? ST_AGC : ST_AGB; break; }
-    if (tv > k) { st = ST_AGM; break; }                  // the first digest has left the ring
-    const unsigned long long o = atomicCAS(a, v, want);  // an older checkpoint: claim the slot
-    if (o == v) break;
-    v = o;
-  }
-  if (st == ST_AGB) st0[ST_AGC * sstride] += 1;          // a mismatch was compared too
-  if (st) st0[st * sstride] += 1;
-}
-
 // Database.Execute (db.go:103-114) when replicas keep the KV: a write's value
 // (its command id) goes to its key and database.version counts it (put,
 // db.go:123-134); a read changes nothing.  The previous value Execute returns
 // is what the key holds at this point of the executed log.
+// Database.Execute's return value (db.go:103-114): the key's value before cmd
+template <int NT>
+__device__ __forceinline__ uint32_t kv_get(const Params& P, Rep<NT>& x, uint32_t cmd) {
+  const uint32_t key = hbm_log(x) ? x.key : wl_key(P, x.kc, cmd);
+  return ldg(&P.kv_val[((size_t)key * nrep<NT>(P) + x.r) * P.C + x.c]);
+}
 template <int NT>
 __device__ __forceinline__ void kv_exec(const Params& P, Rep<NT>& x, uint32_t cmd) {
   if (!wl_write(P, x.kc, cmd)) return;
@@ -397,7 +377,8 @@ __device__ __forceinline__ void paxos_exec(const Params& P, Rep<NT>& x) {     //
     if ((c & (EF_EXISTS | EF_COMMIT)) != (EF_EXISTS | EF_COMMIT)) break;
     if (x.iflags & PAXISIM_F_WOVF) x.flags |= PAXISIM_F_UNFAITHFUL;
     const uint32_t cmd = c & CMD_MASK;
-    if (c & (EF_REQSELF | EF_REQEXT)) request_reply<NT>(P, x, ereq<NT>(P, x, i, c), cmd);
+    if (c & (EF_REQSELF | EF_REQEXT))                             // Reply{Value: p.Execute(cmd)}, paxos.go:352-362
+      request_reply<NT>(P, x, ereq<NT>(P, x, i, c), cmd, P.kv ? kv_get<NT>(P, x, cmd) : 0u);
     x.digest = mix64(x.digest ^ (((uint64_t)(uint32_t)x.execute << 32) | cmd));
     if (P.kv) kv_exec<NT>(P, x, cmd);                              // p.Execute(e.command), paxos.go:352
     set_b(x, i, 0u);                                               // delete(p.log, execute)
@@ -407,11 +388,7 @@ __device__ __forceinline__ void paxos_exec(const Params& P, Rep<NT>& x) {     //
       const size_t ci = ((size_t)k * P.NI + x.inst) * P.C + x.c;
       P.ck_e[ci] = (uint32_t)x.execute;
       P.ck_d[ci] = x.digest;
-      if (P.AR) {
-        const uint32_t kk = (uint32_t)x.execute / CKI;
-        agree_arrive(&P.agr[((size_t)(kk % P.AR) * P.NK + x.key) * P.C + x.c], &P.stats[rc(P, x.r, x.c)],
-                     (size_t)P.N * P.C, kk, x.digest);
-      }
+      if (P.AR) agree_post<NT>(P, x, (uint32_t)x.execute / CKI);
     }
   }
 }
@@ -560,7 +537,7 @@ __device__ __forceinline__ void paxos_handle_p2b(const Params& P, Rep<NT>& x, ui
       if (P.rwc) {
         const uint32_t q = ereq<NT>(P, x, i, c);
         if (!q) { x.flags |= PAXISIM_F_POISON; x.stop = true; return; }   // nil r.Reply
-        request_reply<NT>(P, x, q, req_cid(q));
+        request_reply<NT>(P, x, q, req_cid(q), 0u);   // Reply{Command}: no Value
       } else {
         paxos_exec<NT>(P, x);
       }
@@ -590,7 +567,7 @@ __device__ __forceinline__ void paxos_handle_p3(const Params& P, Rep<NT>& x, uin
     if (P.rwc) {
       if (c & (EF_REQSELF | EF_REQEXT)) {
         const uint32_t q = ereq<NT>(P, x, i, c);
-        request_reply<NT>(P, x, q, req_cid(q));
+        request_reply<NT>(P, x, q, req_cid(q), 0u);   // Reply{Command}: no Value
       }
       return;
     }
@@ -685,7 +662,7 @@ struct PaxosProto {
                                                   uint32_t ri) {
     switch (hdr_type(m.x)) {
       case PAXISIM_MSG_REQUEST: { PXS_CASE_T0 dv_inc<NT>(x, PAXISIM_MSG_REQUEST); handle_request<NT>(P, x, mkreq(m.w, src)); PXS_CASE_T1(PAXISIM_MSG_REQUEST) } break;
-      case PAXISIM_MSG_REPLY: { PXS_CASE_T0 dv_inc<NT>(x, PAXISIM_MSG_REPLY); handle_reply<NT>(P, x, m.w); PXS_CASE_T1(PAXISIM_MSG_REPLY) } break;
+      case PAXISIM_MSG_REPLY: { PXS_CASE_T0 dv_inc<NT>(x, PAXISIM_MSG_REPLY); handle_reply<NT>(P, x, m.w, m.y); PXS_CASE_T1(PAXISIM_MSG_REPLY) } break;
       case PAXISIM_MSG_P1A: { PXS_CASE_T0 dv_inc<NT>(x, PAXISIM_MSG_P1A); paxos_handle_p1a<NT>(P, x, m.y); PXS_CASE_T1(PAXISIM_MSG_P1A) } break;
       case PAXISIM_MSG_P1B: { PXS_CASE_T0 dv_inc<NT>(x, PAXISIM_MSG_P1B); paxos_handle_p1b<NT>(P, x, src, m.y, ri, hdr_n(m.x)); PXS_CASE_T1(PAXISIM_MSG_P1B) } break;
       case PAXISIM_MSG_P2A: { PXS_CASE_T0 dv_inc<NT>(x, PAXISIM_MSG_P2A); paxos_handle_p2a<NT>(P, x, m.y, (int32_t)m.z, m.w); PXS_CASE_T1(PAXISIM_MSG_P2A) } break;

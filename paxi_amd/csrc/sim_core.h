@@ -49,6 +49,7 @@ struct Rep {
   // LDS views
   uint32_t *l_a, *l_b, *l_c, *l_wcur, *l_wiss, *l_poison;
   uint8_t* l_cnt;
+  uint8_t* l_agn;                       // agreement-ring arrivals this step, [parity][r][lane] (agree_post)
   uint4* rec;                           // this block's record region
 };
 
@@ -332,15 +333,17 @@ __device__ __forceinline__ bool wl_write(const Params& P, uint32_t kc, uint32_t 
   return ppm_hit(fmix32(wl_hash(kc, cid) ^ 0x27D4EB2Fu), P.write_ppm);
 }
 
-// The HTTP response reaches worker w, which issues its next request: it
+// The HTTP response reaches worker w, which keeps its Reply.Value (the value
+// a read returned, benchmark.go:259-262) and issues its next request: it
 // arrives at the worker's target (client source N) in the next step.
 template <int NT>
-__device__ __forceinline__ void client_reply(const Params& P, Rep<NT>& x, uint32_t cid) {
+__device__ __forceinline__ void client_reply(const Params& P, Rep<NT>& x, uint32_t cid, uint32_t value) {
   uint32_t w = (cid - 1u) - P.WK * __umulhi(cid - 1u, P.wk_magic);   // (cid-1) % WK
   if (w >= P.WK) w -= P.WK;
   const uint32_t wi = (w << 6) | x.lane;
   if (x.l_wcur[wi] != cid) return;              // duplicate reply: the worker moved on
   x.replies++;
+  P.wrep[(size_t)w * P.C + x.c] = value;
   const uint32_t issued = x.l_wiss[wi];
   if (P.max_requests == 0 || issued < P.max_requests) {
     const uint64_t nc = 1ull + w + (uint64_t)P.WK * issued;
@@ -767,6 +770,64 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
 }
 
 // ---------------------------------------------------------------------------
+// Agreement ring (client.go:279-320 Consensus, restated as a running check,
+// DESIGN.md §3.9): every CKI executed slots a replica reaches digest
+// checkpoint k; the first replica to reach it records its digest in the
+// cluster's ring, every later one compares.  Arrivals are applied in a fixed
+// order, so the coverage counters do not depend on which wave runs first:
+// during a step each replica appends its arrivals to its own list (agree_post),
+// and after the step's barrier one wave applies every replica's list in
+// replica index order (agree_drain) - the order in which the oracle, which runs
+// the replicas of a step one after another, applies them.  Lists alternate by
+// step parity, so the next step's arrivals never meet the drain.  A replica
+// that reaches more than AGMAX checkpoints in one step counts the extra ones
+// as missed (both backends).
+// ---------------------------------------------------------------------------
+template <int NT>
+__device__ __forceinline__ void agree_post(const Params& P, Rep<NT>& x, uint32_t k) {
+  const uint32_t par = x.t & 1u;
+  uint8_t* cp = &x.l_agn[((par * nrep<NT>(P) + x.r) << 6) | x.lane];
+  const uint32_t n = *cp;
+  if (n < AGMAX) {
+    const uint64_t d = x.digest;
+    const uint64_t want = ((uint64_t)k << 40) | ((d ^ (d >> 24)) & 0xFFFFFFFFFFull);
+    P.agq[(((size_t)par * AGMAX + n) * nrep<NT>(P) + x.r) * P.C + x.c] =
+        make_uint4((uint32_t)want, (uint32_t)(want >> 32), x.key, 0u);
+  }
+  if (n < 255u) *cp = (uint8_t)(n + 1u);
+}
+template <int NT>
+__device__ __forceinline__ void agree_drain(const Params& P, const Rep<NT>& x, uint32_t par) {
+  const uint32_t N = nrep<NT>(P);
+  for (uint32_t r = 0; r < N; r++) {
+    uint8_t* cp = &x.l_agn[((par * N + r) << 6) | x.lane];
+    const uint32_t n = *cp;
+    if (!n) continue;
+    *cp = 0;
+    uint32_t cmp = 0, miss = n > AGMAX ? n - AGMAX : 0u, bad = 0;
+    for (uint32_t j = 0; j < n && j < AGMAX; j++) {
+      const uint4 e = P.agq[(((size_t)par * AGMAX + j) * N + r) * P.C + x.c];
+      const unsigned long long want = (unsigned long long)e.x | ((unsigned long long)e.y << 32);
+      const uint32_t k = e.y >> 8;
+      unsigned long long* a = &P.agr[((size_t)(k % P.AR) * P.NK + e.z) * P.C + x.c];
+      const unsigned long long v = *a;
+      const uint32_t tv = (uint32_t)(v >> 40);
+      if (v == 0ull || tv < k) {
+        *a = want;                                       // first to arrive (or an older checkpoint left): record
+      } else if (tv > k) {
+        miss++;                                          // the first digest has left the ring
+      } else {
+        cmp++;
+        bad += v != want;
+      }
+    }
+    if (cmp) P.stats[krc(P, ST_AGC, r, x.c)] += cmp;
+    if (miss) P.stats[krc(P, ST_AGM, r, x.c)] += miss;
+    if (bad) P.stats[krc(P, ST_AGB, r, x.c)] += bad;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // The step kernel: stage the LDS image, run S steps, write everything back.
 // ---------------------------------------------------------------------------
 // Waves per SIMD the register allocator must allow.  The dispatcher places a
@@ -833,7 +894,10 @@ __global__ void __launch_bounds__(max_threads<NT>(), min_waves<NT>()) sim_steps(
   x.l_wiss = reinterpret_cast<uint32_t*>(L + P.img.off_wiss);
   x.l_poison = reinterpret_cast<uint32_t*>(L + P.img.off_poison);
   x.l_cnt = L + P.img.off_cnt;
+  x.l_agn = L + P.off_agn;
   x.rec = P.rec + (size_t)blk * P.rec_per_block;
+  if (P.AR)   // this launch's arrival counts (drained every step, so they start empty)
+    for (uint32_t k = (wave - grp * N) * LANES + x.lane; k < 2u * N * LANES; k += N * LANES) x.l_agn[k] = 0;
   const bool live = x.c < bound && x.r < N;
   // the log layout is a constant of the instance (paxos_kernel.h: hbm_log)
   x.es = Proto::kind == PAXISIM_WPAXOS ? 4u : LANES;
@@ -879,6 +943,7 @@ __global__ void __launch_bounds__(max_threads<NT>(), min_waves<NT>()) sim_steps(
     st.barrier += stamp() - sb;
     st.steps++;
 #endif
+    if (P.AR && live && x.r == N - 1u) agree_drain<NT>(P, x, t & 1u);   // this step's arrivals, replica order
   }
 #ifdef PXS_STAMPS
   if (x.lane == 0 && P.dbg) {

@@ -244,7 +244,7 @@ struct WPaxosProto {
     if (type == PAXISIM_MSG_REPLY) {                                   // node.recv (node.go:83-90)
       PXS_CASE_T0
       dv_inc<NT>(x, PAXISIM_MSG_REPLY);
-      handle_reply<NT>(P, x, m.w);
+      handle_reply<NT>(P, x, m.w, m.y);
       PXS_CASE_T1(PAXISIM_MSG_REPLY)
       return;
     }

@@ -56,3 +56,32 @@ def stats_counters(delta, alg_bytes=0, violations=0, flagged=None, **extra):
     d.update(extra)
     d.update({"flag_" + n: flagged[i] for i, n in enumerate(FLAG_NAMES)})
     return d
+
+
+# ---- sharding invariance (per-cluster state at G=8 equals G=1) ----
+DIGEST_CLUSTERS = 256
+
+
+def digest_range(clusters_per_rank):
+    """Local clusters each rank digests: [C/2, C/2 + 256) (clipped to the shard)."""
+    lo = clusters_per_rank // 2
+    return lo, max(0, min(DIGEST_CLUSTERS, clusters_per_rank - lo))
+
+
+def state_digest(sim, lo, n):
+    """SHA-256 (first 16 hex digits) of the replica states of local clusters
+    [lo, lo+n) as paxisim_read_state returns them: equal digests, equal states."""
+    import hashlib
+    if n == 0:
+        return "0" * 16
+    return hashlib.sha256(bytes(sim.read_state(lo, n))).hexdigest()[:16]
+
+
+def gather_digests(digest, world):
+    """{rank: digest} on every rank (torch.distributed all_gather_object)."""
+    if world == 1:
+        return {0: digest}
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, digest)
+    return {r: d for r, d in enumerate(out)}

@@ -22,6 +22,13 @@ class PaxisimError(RuntimeError):
     pass
 
 
+def quorum(cfg, kind, ack_mask):
+    """paxisim_quorum: the kernels' quorum predicate (quorum.go:55-119) for cfg's zones; host only."""
+    ok = C.c_int()
+    _check(load_library().paxisim_quorum(C.byref(cfg), kind, ack_mask, C.byref(ok)))
+    return bool(ok.value)
+
+
 def load_library():
     """Load the in-tree HIP library; raise if it is absent (no fallback)."""
     global _lib
@@ -48,6 +55,11 @@ def load_library():
     L.paxisim_occupancy.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     L.paxisim_active_clusters.restype = C.c_int
     L.paxisim_active_clusters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+    L.paxisim_quorum.restype = C.c_int
+    L.paxisim_quorum.argtypes = [C.POINTER(abi.Config), C.c_uint32, C.c_uint32, C.POINTER(C.c_int)]
+    L.paxisim_read_client.restype = C.c_int
+    L.paxisim_read_client.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(abi.WorkerState), C.c_uint32,
+                                      C.POINTER(C.c_uint32)]
     L.paxisim_read_activity.restype = C.c_int
     L.paxisim_read_activity.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint32)]
     L.paxisim_device_bytes.restype = C.c_int
@@ -78,7 +90,7 @@ EXPORTED = ["paxisim_abi_version", "paxisim_last_error", "paxisim_create", "paxi
             "paxisim_fault_add", "paxisim_step", "paxisim_sync", "paxisim_stats_get",
             "paxisim_read_state", "paxisim_read_instances", "paxisim_check", "paxisim_kernel_time", "paxisim_device_bytes",
             "paxisim_linearizable", "paxisim_history", "paxisim_occupancy", "paxisim_inject", "paxisim_read_log",
-            "paxisim_history_load", "paxisim_active_clusters", "paxisim_read_activity", "paxisim_dist_init", "paxisim_dist_unique_id",
+            "paxisim_history_load", "paxisim_active_clusters", "paxisim_read_activity", "paxisim_read_client", "paxisim_quorum", "paxisim_dist_init", "paxisim_dist_unique_id",
             "paxisim_dist_init_rank", "paxisim_dist_allreduce", "paxisim_dist_stats", "paxisim_dist_destroy",
             "paxisim_read_kv", "paxisim_read_inbox", "paxisim_deliver", "paxisim_commands"]
 
@@ -97,6 +109,13 @@ def _read_inbox(fn, h, cluster, replica, check):
         if n.value <= cap:
             return [arr[i].as_tuple() for i in range(n.value)]
         cap = n.value
+
+
+def _read_client(fn, h, cluster, n, check):
+    arr = (abi.WorkerState * max(1, n))()
+    got = C.c_uint32()
+    check(fn(h, cluster, arr, n, C.byref(got)))
+    return [arr[i].as_tuple() for i in range(min(n, got.value))]
 
 
 class Simulation:
@@ -184,6 +203,10 @@ class Simulation:
         buf = (C.c_uint32 * max(1, 5 * n.value))()
         _check(load_library().paxisim_history(self.h, cluster, buf, n.value, C.byref(n)))
         return [tuple(buf[5 * i: 5 * i + 5]) for i in range(n.value)]
+
+    def read_client(self, cluster):
+        """[(cid, issued, reply_value)] of the cluster's closed-loop workers (paxisim_read_client)."""
+        return _read_client(load_library().paxisim_read_client, self.h, cluster, self.wl.outstanding, _check)
 
     def read_kv(self, cluster, replica, n):
         """Database.Get (db.go:116-121) of keys [0, n) of one replica (paxisim_read_kv)."""

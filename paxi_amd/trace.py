@@ -23,7 +23,8 @@ message as a gob stream, one `gob.Encoder` per connection
 Messages map to Paxi values as follows (a ballot is the 64-bit
 `n << 32 | zone << 16 | node`, an ID is "zone.node"):
   Request  paxi.Request{Command, NodeID = forwarder}          (node.go:165-172)
-  Reply    paxi.Reply{Command}                                 (node.go:83-97)
+  Reply    paxi.Reply{Command, Value}                          (node.go:83-97; Value = Execute's result,
+           paxos.go:352-362, as a write's value: Uvarint(cid) in 10 bytes, nil = 0)
   P1a..P3  paxos.P1a{Ballot} / P1b{Ballot, ID, Log} / P2a{Ballot, Slot, Command} /
            P2b{Ballot, ID, Slot} / P3{Ballot, Slot, Command}   (paxos/msg.go:19-70)
   ABD      abd.Get{ID, CID, Key} / GetReply{ID, CID, Key, Value, Version} /
@@ -36,7 +37,7 @@ for a write (client/client.go:42-45) or nil for a read, ClientID "", CommandID
 = cid}; the simulator derives key and kind from the command id
 (paxisim_commands), so an imported command must agree with them.  Not carried
 (the simulator has no such state): a Request's Timestamp and Properties, a
-Reply's Value / Properties / Err.
+Reply's Properties / Err.
   EPaxos   epaxos.PreAccept / PreAcceptReply / Accept / AcceptReply / Commit (epaxos/msg.go:18-65)
 """
 from __future__ import annotations
@@ -186,7 +187,7 @@ class Codec:
         if t == T_REQUEST:
             return f"{P}.Request", {"Command": self.command(cid), "NodeID": top.id(src)}
         if t == T_REPLY:
-            return f"{P}.Reply", {"Command": self.command(cid)}
+            return f"{P}.Reply", {"Command": self.command(cid), "Value": uvarint10(b) if b else None}
         if self.proto == abi.EPAXOS:
             return self._ep_to_go(src, t, b, s, cid, [w for r in recs[1:] for w in r[1:]])
         if self.proto == abi.ABD:
@@ -267,7 +268,8 @@ class Codec:
         if t == T_REQUEST:
             return [(src, T_REQUEST, 0, 0, self.check_command(v["Command"]))]
         if t == T_REPLY:
-            return [(src, T_REPLY, 0, 0, self.check_command(v["Command"]))]
+            val = v.get("Value")
+            return [(src, T_REPLY, read_uvarint(val) if val else 0, 0, self.check_command(v["Command"]))]
         if self.proto == abi.EPAXOS:
             if name not in EPAXOS_NAMES.values():
                 raise TraceError(f"{name} is not an EPaxos message")

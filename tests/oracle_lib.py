@@ -126,6 +126,12 @@ class OracleSim:
         _check(lib().oracle_history(self.h, cluster, buf, n.value, C.byref(n)))
         return [tuple(buf[5 * i: 5 * i + 5]) for i in range(n.value)]
 
+    def read_client(self, cluster):
+        from paxi_amd.sim import _read_client
+        lib().oracle_read_client.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(abi.WorkerState), C.c_uint32,
+                                             C.POINTER(C.c_uint32)]
+        return _read_client(lib().oracle_read_client, self.h, cluster, self.wl.outstanding, _check)
+
     def read_kv(self, cluster, replica, n):
         buf = (C.c_uint32 * max(1, n))()
         _check(lib().oracle_read_kv(self.h, cluster, replica, buf, n))

@@ -74,3 +74,18 @@ def test_create_without_gpu_fails_loudly():
     from paxi_amd import abi, sim
     with pytest.raises(sim.PaxisimError):
         sim.Simulation(abi.make_config(clusters=4), abi.make_workload())
+
+
+def test_quorum_predicates_match_the_oracle():
+    """paxisim_quorum (the kernels' own predicate, built for the host) equals the
+    oracle's restatement of quorum.go:55-119 for every kind, mask and layout."""
+    import oracle_lib as ol
+    from paxi_amd import abi, sim
+    for npz in ([3], [5], [2, 2], [3, 3, 3], [2, 3, 4], [4, 4, 4, 4]):
+        for fz in (0, 1, 2):
+            cfg = abi.make_config(npz=npz, fz=fz)
+            n = sum(npz)
+            masks = range(1 << n) if n <= 9 else range(0, 1 << n, 37)
+            for kind in range(8):
+                for m in masks:
+                    assert sim.quorum(cfg, kind, m) == ol.quorum(kind, npz, m, fz), (npz, fz, kind, m)

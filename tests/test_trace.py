@@ -360,3 +360,18 @@ def test_gob_omitted_float_and_complex_fields_decode_as_zero():
         assert gob.full(t, {"X": 3}) == {"X": 3, "F": 0.0, "Z": 0j}
     finally:
         del gob.REGISTERED[name]
+
+
+def test_reply_value_travels_in_the_trace():
+    """A forwarded request's Reply carries Execute's value (paxos.go:352-362)
+    over the wire back to the forwarder, and import restores it."""
+    cfg, wl, fp = paxos_case()
+    wl.target[1] = 2                                          # a worker at a follower: its requests are forwarded
+    a = OracleSim(cfg, wl, fp)
+    tr = trace.capture(a, 1, 120)
+    streams, sched = trace.export(a, 1, tr)
+    vals = [v["Value"] for data in streams.values() for n, v in gob.Decoder(data) if n == f"{P}.Reply"]
+    assert vals and any(x is not None for x in vals)
+    back = trace.import_streams(a, 1, streams, sched)
+    reps = [r for (t, s, d, recs) in back["msgs"] for r in recs if r[1] == trace.T_REPLY]
+    assert any(r[2] for r in reps)
