@@ -42,7 +42,8 @@ METRIC = "sim messages delivered/sec + committed slots/sec, 1M Paxos clusters, 1
 FLAG_NAMES = ("WOVF", "GHOST", "MBOX_OVF", "PEND_OVF", "UNFAITHFUL", "POISON", "BALLOT_OVF", "HIST_OVF")
 
 # per-config defaults: clusters per GPU, virtual steps per bench step, window, mailbox capacity
-DEFAULTS = {2: dict(clusters=1 << 20, sim_steps=400, window=16, mbox=32),
+DEFAULTS = {1: dict(clusters=1, sim_steps=3010, window=32, mbox=16),
+            2: dict(clusters=1 << 20, sim_steps=400, window=16, mbox=32),
             3: dict(clusters=1 << 20, sim_steps=80, window=16, mbox=16),
             4: dict(clusters=1 << 19, sim_steps=200, window=16, mbox=24),
             5: dict(clusters=1 << 18, sim_steps=200, window=16, mbox=24)}
@@ -73,6 +74,16 @@ def build_id():
 def workload(cfg_id, clusters, base, device, args):
     """(cfg, workload, fault process, scripted faults, description) of a BASELINE config."""
     from paxi_amd import abi
+    if cfg_id == 1:
+        # the reference's own CPU case (bin/simulation.sh): 3 replicas, one
+        # client, 1000 sequential writes to 1.1, no faults; 3 steps a request
+        cfg = abi.make_config(npz=[3], clusters=clusters, cluster_base=base, seed=1, window=args.window,
+                              mbox_cap=args.mbox, max_delay=0, steps_per_launch=LAUNCH_STEPS, device=device,
+                              kv=args.kv)
+        wl = abi.make_workload(outstanding=1, max_requests=1000, target=[0])
+        return cfg, wl, None, [], {
+            "workload": "BASELINE config 1: Multi-Paxos 3 replicas, 1 client, 1000 writes, no faults "
+                        "(the reference's CPU case; run with --warmup 0 --steps 1)", "replicas": 3, "outstanding": 1}
     if cfg_id == 2:
         cfg = abi.make_config(npz=[5], clusters=clusters, cluster_base=base, seed=42, window=args.window,
                               mbox_cap=args.mbox, max_delay=4, steps_per_launch=LAUNCH_STEPS, device=device,
@@ -265,7 +276,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5])
     ap.add_argument("--clusters", type=int, default=None, help="clusters per GPU (default: the config's)")
     ap.add_argument("--sim-steps", type=int, default=None, help="virtual steps per bench step")
     ap.add_argument("--window", type=int, default=None)

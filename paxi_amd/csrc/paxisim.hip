@@ -97,11 +97,8 @@ __global__ void init_kernel(Params P) {
     for (uint32_t r = 0; r < P.N; r++) P.slot[rc(P, r, c)] = 0xFFFFFFFFu;   // slot: -1 (paxos.go:45)
   if (P.protocol == PAXISIM_WPAXOS)                                         // fresh kpaxos instances
     for (uint32_t k = 0; k < P.keys; k++)
-      for (uint32_t r = 0; r < P.N; r++) {
-        const size_t si = (((size_t)blk * P.keys + k) * P.N + r) * LANES + lane;
-        P.wst[2 * si] = make_uint4(0u, 0xFFFFFFFFu, 0u, 0u);
-        P.wst[2 * si + 1] = make_uint4(0u, 0u, 0u, POL_NONE);
-      }
+      for (uint32_t r = 0; r < P.N; r++)
+        wp_write(P, blk, k, r, lane, make_uint4(0u, 0xFFFFFFFFu, 0u, 0u), make_uint4(0u, 0u, 0u, POL_NONE));
   if (P.protocol == PAXISIM_EPAXOS) {                                      // replica.go:37-47: -1 everywhere
     for (uint32_t k = 0; k < 3 * P.N * P.N; k++) P.ep_sce[(size_t)k * P.C + c] = 0xFFFFFFFFu;
     for (uint32_t k = 0; k < P.N * P.keys * P.N; k++) P.ep_cf[(size_t)k * P.C + c] = 0xFFFFFFFFu;
@@ -208,8 +205,8 @@ __global__ void gather_kernel(Params P, uint64_t lo, uint64_t n, paxisim_replica
     uint32_t hi = 0, led = 0, act = 0, ex = 0, np = 0, em = 0;
     uint64_t d = 0;
     for (uint32_t k = 0; k < P.keys; k++) {
-      const size_t si = (((c / LANES) * P.keys + k) * P.N + r) * LANES + (c % LANES);
-      const uint4 a = P.wst[2 * si], b = P.wst[2 * si + 1];
+      uint4 a, b;
+      wp_read(P, c / LANES, k, r, (uint32_t)(c % LANES), a, b);
       const uint32_t exists = (a.w >> 1) & 1u;
       hi = a.x > hi ? a.x : hi;
       led += exists && ((a.w & 1u) || bal_id(a.x) == r);    // Replica.keys() replica.go:110-118
@@ -257,7 +254,8 @@ __global__ void gather_inst_kernel(Params P, uint64_t lo, uint64_t n, paxisim_in
   memset(&s, 0, sizeof s);
   if (P.protocol == PAXISIM_WPAXOS) {
     const size_t si = (((c / LANES) * P.keys + k) * P.N + r) * LANES + (c % LANES);
-    const uint4 a = P.wst[2 * si], b = P.wst[2 * si + 1];
+    uint4 a, b;
+    wp_read(P, c / LANES, k, r, (uint32_t)(c % LANES), a, b);
     s.ballot = a.x;
     s.slot = (int32_t)a.y;
     s.execute = (int32_t)a.z;
@@ -307,8 +305,8 @@ __global__ void check_kernel(Params P, uint64_t* out) {
     for (uint32_t r = 0; r < P.N; r++) bad |= P.stats[krc(P, ST_AGB, r, c)] != 0;   // running check (paxos_exec)
     auto exec_digest = [&](uint32_t key, uint32_t r, uint32_t& e, uint64_t& d) {
       if (P.protocol == PAXISIM_WPAXOS) {
-        const size_t si = (((c / LANES) * P.keys + key) * P.N + r) * LANES + (c % LANES);
-        const uint4 a = P.wst[2 * si], b = P.wst[2 * si + 1];
+        uint4 a, b;
+        wp_read(P, c / LANES, key, r, (uint32_t)(c % LANES), a, b);
         e = a.z;
         d = (uint64_t)b.y | ((uint64_t)b.z << 32);
       } else {
@@ -422,7 +420,9 @@ __global__ void read_log_kernel(Params P, uint64_t cl, uint32_t r, uint32_t key,
   const uint32_t w = (uint32_t)s & (P.W - 1u);
   if (P.protocol == PAXISIM_WPAXOS) {
     const size_t si = (((size_t)blk * P.keys + key) * P.N + r) * LANES + lane;
-    execute = (int32_t)P.wst[2 * si].z;
+    uint4 a, b;
+    wp_read(P, blk, key, r, lane, a, b);
+    execute = (int32_t)a.z;
     const uint32_t* e = P.wlog + (si * P.W + w) * 4u;
     eb = e[0]; ec = e[1]; ea = e[2]; ex = e[3];
   } else {
@@ -645,12 +645,15 @@ __global__ void replay_kernel(Params P, uint64_t s0, uint64_t s1, uint32_t tnow)
 // ---------------------------------------------------------------------------
 // C-ABI
 // ---------------------------------------------------------------------------
-static Image proto_image(uint32_t protocol, uint32_t N, uint32_t W, uint32_t K, uint32_t WK, uint32_t D) {
+static Image proto_image(uint32_t protocol, uint32_t N, uint32_t W, uint32_t K, uint32_t WK, uint32_t D,
+                         uint32_t wlds) {
   if (protocol == PAXISIM_ABD) {
     const uint32_t kv = N * K * LANES * 4u;
     return image_layout(kv, kv, N * abd_ow(WK) * ABD_OPF * LANES * 4u, N, WK, D);
   }
-  if (protocol == PAXISIM_WPAXOS || protocol == PAXISIM_EPAXOS) return image_layout(0, 0, 0, N, WK, D);   // state in HBM
+  if (protocol == PAXISIM_WPAXOS)   // instance scalars in the image (wlds), or all in HBM
+    return image_layout(wlds ? K * N * WP_WORDS * LANES * 4u : 0u, 0, 0, N, WK, D);
+  if (protocol == PAXISIM_EPAXOS) return image_layout(0, 0, 0, N, WK, D);   // state in HBM
   const uint32_t logb = N * W * LANES * 4u;
   return image_layout(logb, logb, logb, N, WK, D);
 }
@@ -696,7 +699,7 @@ static int check_config(const paxisim_config* cfg, const paxisim_workload* wl, c
     if (wl->target[w] >= N) return fail(PAXISIM_EINVAL, "target[%u]", w);
   if (fp->slow_ppm && (fp->slow_min > fp->slow_max || fp->slow_max > cfg->max_delay))
     return fail(PAXISIM_EINVAL, "slow delay range exceeds max_delay");
-  const Image img = proto_image(cfg->protocol, N, cfg->window, cfg->keys, wl->outstanding, cfg->max_delay + 2u);
+  const Image img = proto_image(cfg->protocol, N, cfg->window, cfg->keys, wl->outstanding, cfg->max_delay + 2u, 0);
   if (img.bytes > LDS_MAX)
     return fail(PAXISIM_EUNSUPP, "workgroup image %u B exceeds LDS (%u B): reduce window/max_delay/replicas",
                 img.bytes, LDS_MAX);
@@ -739,8 +742,8 @@ extern "C" int paxisim_destroy(paxisim* h) {
   return 0;
 }
 
-static StepOps step_ops_for(uint32_t protocol, uint32_t N) {
-  if (protocol == PAXISIM_WPAXOS) return wpaxos_step_ops(N);
+static StepOps step_ops_for(uint32_t protocol, uint32_t N, bool wlds) {
+  if (protocol == PAXISIM_WPAXOS) return wpaxos_step_ops(N, wlds);
   if (protocol == PAXISIM_ABD) return abd_step_ops(N);
   if (protocol == PAXISIM_EPAXOS) return epaxos_step_ops(N);
   return paxos_step_ops(N);
@@ -861,13 +864,20 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     P.wnk[w] = z < P.keys ? (P.keys - z + P.Z - 1u) / P.Z : 0u;
     P.wnk_magic[w] = P.wnk[w] ? 0xFFFFFFFFu / P.wnk[w] : 0u;
   }
-  P.img = proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D);
+  // WPaxos: the instance scalars move into the tile image when one tile's
+  // image (and the agreement counts) fits the LDS; PAXISIM_WLDS=0 keeps them in HBM (A/B)
+  if (P.protocol == PAXISIM_WPAXOS) {
+    const char* ev = getenv("PAXISIM_WLDS");
+    const uint32_t agn = P.AR ? (2u * N * LANES + 15u) & ~15u : 0u;
+    P.wlds = !(ev && atoi(ev) == 0) && proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D, 1).bytes + agn <= LDS_MAX;
+  }
+  P.img = proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D, P.wlds);
   {
     // Cluster groups per workgroup (sim_core.h): as many 64-cluster tiles as
     // the step kernel's registers leave wave slots for on every SIMD
     // (ceil(G*N/4) <= waves per SIMD) and the LDS holds, at most 4.
     int vgprs = 0, maxthr = 0;
-    h->ops = step_ops_for(P.protocol, N);
+    h->ops = step_ops_for(P.protocol, N, P.wlds != 0);
     if (h->ops.attrs(&vgprs, &maxthr) != hipSuccess || vgprs <= 0) vgprs = 512;
     if (maxthr <= 0) maxthr = (int)(N * LANES);
     const uint32_t alloc = ((uint32_t)vgprs + 7u) / 8u * 8u;
@@ -909,7 +919,8 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     uint4* gst = carve<uint4>(p, NIC * GMAX);
     uint32_t* st = carve<uint32_t>(p, NC * NSTAT);
     uint32_t* reqx = carve<uint32_t>(p, wp ? 0 : NC * P.W);
-    uint4* wst = carve<uint4>(p, wp ? NIC * 2 : 0);
+    uint4* wst = carve<uint4>(p, wp && !P.wlds ? NIC * 2 : 0);
+    uint64_t* wdig = carve<uint64_t>(p, wp && P.wlds ? NIC : 0);
     uint32_t* wlog = carve<uint32_t>(p, wp ? NIC * P.W * 4 : 0);
     uint32_t* wpend = carve<uint32_t>(p, wp ? NIC * PMAX : 0);
     uint4* wpx = carve<uint4>(p, wp && cfg->policy != PAXISIM_POLICY_CONSECUTIVE ? NIC * 3 : 0);
@@ -934,7 +945,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
       P.digest = dg; P.kc = kc; P.pend = pend; P.fwd = fwd;
       P.link_drop = links; P.link_slow = links + NC * N;
       P.ck_e = cke; P.ck_d = ckd; P.stats = st; P.reqx = reqx; P.hist = hist; P.image = image; P.rec = rec;
-      P.wst = wst; P.wlog = wlog; P.wpend = wpend; P.gst = gst; P.wpx = wpx;
+      P.wst = wst; P.wdig = wdig; P.wlog = wlog; P.wpend = wpend; P.gst = gst; P.wpx = wpx;
       P.slot_of = maps; P.cl_of = maps + C; P.frz = maps + 2 * C; P.qf = maps + 3 * C;
       P.agr = agr;
       P.agq = agq;

@@ -140,7 +140,9 @@ struct Params {
   // WPaxos kpaxos instances, one 32-B state + a W-entry window + PMAX pending per
   // (blk, key, r, lane): {ballot, slot, execute, active|exists<<1|p1acks<<16,
   // npend, digest lo, digest hi, policy last|hits<<8}; entries {ballot, cmd|flags, acks, request}
-  uint4* wst;            // [blk][K][N][64][2]
+  uint4* wst;            // [blk][K][N][64][2] (wlds = 0)
+  uint32_t wlds;         // 1: instance scalars in the tile image (region a, LDS during a launch), digests in wdig
+  uint64_t* wdig;        // [blk][K][N][64] instance digests (wlds = 1)
   uint32_t* wlog;        // [blk][K][N][64][W][4]
   uint32_t* wpend;       // [blk][K][N][64][PMAX]
   uint4* wpx;            // [blk][K][N][64][3] majority {hits u16 x 16 (2 x uint4), {sum, start step}} / ema {s lo, s hi, zone}
@@ -179,6 +181,46 @@ struct Params {
   uint32_t* kv_ver;      // [r][C] database.version
   uint32_t* wrep;        // [WK][C] Reply.Value of each worker's last reply (0 = nil)
 };
+
+// Persistent scalars of the kpaxos instance (blk, k, r, lane) in the record
+// form {a = ballot, slot, execute, active|exists<<1|wovf,ghost<<2|p1acks<<16;
+// b = npend, digest lo, digest hi, policy|committed window<<16}, from either
+// layout: the HBM table wst, or (wlds) five words in the tile image,
+// [(k*N + r)*5 + word][lane] = {ballot, slot, execute, meta | npend << 4,
+// policy | committed window << 16}, and the digest in wdig.
+constexpr uint32_t WP_WORDS = 5;
+__device__ __forceinline__ size_t wp_si(const Params& P, uint64_t blk, uint32_t k, uint32_t r, uint32_t lane) {
+  return ((blk * P.keys + k) * P.N + r) * 64u + lane;
+}
+__device__ __forceinline__ uint32_t* wp_img(const Params& P, uint64_t blk, uint32_t k, uint32_t r, uint32_t lane) {
+  return reinterpret_cast<uint32_t*>(P.image + (size_t)blk * P.img.bytes + P.img.off_a) +
+         ((size_t)(k * P.N + r) * WP_WORDS << 6) + lane;
+}
+__device__ __forceinline__ void wp_read(const Params& P, uint64_t blk, uint32_t k, uint32_t r, uint32_t lane, uint4& a,
+                                        uint4& b) {
+  const size_t si = wp_si(P, blk, k, r, lane);
+  if (!P.wlds) {
+    a = P.wst[2 * si];
+    b = P.wst[2 * si + 1];
+    return;
+  }
+  const uint32_t* w = wp_img(P, blk, k, r, lane);
+  const uint64_t d = P.wdig[si];
+  a = make_uint4(w[0], w[64], w[128], w[192] & 0xFFFF000Fu);
+  b = make_uint4((w[192] >> 4) & 0x3Fu, (uint32_t)d, (uint32_t)(d >> 32), w[256]);
+}
+__device__ __forceinline__ void wp_write(const Params& P, uint64_t blk, uint32_t k, uint32_t r, uint32_t lane,
+                                         const uint4& a, const uint4& b) {
+  const size_t si = wp_si(P, blk, k, r, lane);
+  if (!P.wlds) {
+    P.wst[2 * si] = a;
+    P.wst[2 * si + 1] = b;
+    return;
+  }
+  uint32_t* w = wp_img(P, blk, k, r, lane);
+  w[0] = a.x; w[64] = a.y; w[128] = a.z; w[192] = (a.w & 0xFFFF000Fu) | (b.x << 4); w[256] = b.w;
+  P.wdig[si] = (uint64_t)b.y | ((uint64_t)b.z << 32);
+}
 
 // slot of local cluster c
 __device__ __forceinline__ uint64_t slot_of(const Params& P, uint64_t c) { return P.slot_of[c]; }

@@ -351,11 +351,24 @@ __device__ __forceinline__ void handle_request(const Params& P, Rep<NT>& x, uint
 // (its command id) goes to its key and database.version counts it (put,
 // db.go:123-134); a read changes nothing.  The previous value Execute returns
 // is what the key holds at this point of the executed log.
-// Database.Execute's return value (db.go:103-114): the key's value before cmd
+// Database.Execute's return value (db.go:103-114): the key's value before cmd.
+// A plain load: only the reply's store consumes it, so the wait for it lands
+// there rather than here (PXS_KV_LDG=1: wait at once, A/B).
+#ifndef PXS_KV_LDG
+#define PXS_KV_LDG 0
+#endif
+#ifndef PXS_AGREE_POST
+#define PXS_AGREE_POST 1    // 0: no agreement-ring arrivals (A/B attribution only)
+#endif
+#ifndef PXS_REPLY_VALUE
+#define PXS_REPLY_VALUE 1   // 0: replies carry no value (A/B attribution only; not the reference's behaviour)
+#endif
 template <int NT>
 __device__ __forceinline__ uint32_t kv_get(const Params& P, Rep<NT>& x, uint32_t cmd) {
+  if (!PXS_REPLY_VALUE) return 0u;
   const uint32_t key = hbm_log(x) ? x.key : wl_key(P, x.kc, cmd);
-  return ldg(&P.kv_val[((size_t)key * nrep<NT>(P) + x.r) * P.C + x.c]);
+  const uint32_t* a = &P.kv_val[((size_t)key * nrep<NT>(P) + x.r) * P.C + x.c];
+  return PXS_KV_LDG ? ldg(a) : *a;
 }
 template <int NT>
 __device__ __forceinline__ void kv_exec(const Params& P, Rep<NT>& x, uint32_t cmd) {
@@ -388,7 +401,7 @@ __device__ __forceinline__ void paxos_exec(const Params& P, Rep<NT>& x) {     //
       const size_t ci = ((size_t)k * P.NI + x.inst) * P.C + x.c;
       P.ck_e[ci] = (uint32_t)x.execute;
       P.ck_d[ci] = x.digest;
-      if (P.AR) agree_post<NT>(P, x, (uint32_t)x.execute / CKI);
+      if (P.AR && PXS_AGREE_POST) agree_post<NT>(P, x, (uint32_t)x.execute / CKI);
     }
   }
 }

@@ -50,6 +50,7 @@ struct Rep {
   uint32_t *l_a, *l_b, *l_c, *l_wcur, *l_wiss, *l_poison;
   uint8_t* l_cnt;
   uint8_t* l_agn;                       // agreement-ring arrivals this step, [parity][r][lane] (agree_post)
+  uint32_t* l_inst;                     // WPaxos (wlds): instance scalars in LDS (wpaxos_kernel.h)
   uint4* rec;                           // this block's record region
 };
 
@@ -333,6 +334,9 @@ __device__ __forceinline__ bool wl_write(const Params& P, uint32_t kc, uint32_t 
   return ppm_hit(fmix32(wl_hash(kc, cid) ^ 0x27D4EB2Fu), P.write_ppm);
 }
 
+#ifndef PXS_REPLY_STORE
+#define PXS_REPLY_STORE 1   // 0: the worker's last Reply.Value is not kept (A/B attribution only)
+#endif
 // The HTTP response reaches worker w, which keeps its Reply.Value (the value
 // a read returned, benchmark.go:259-262) and issues its next request: it
 // arrives at the worker's target (client source N) in the next step.
@@ -343,7 +347,7 @@ __device__ __forceinline__ void client_reply(const Params& P, Rep<NT>& x, uint32
   const uint32_t wi = (w << 6) | x.lane;
   if (x.l_wcur[wi] != cid) return;              // duplicate reply: the worker moved on
   x.replies++;
-  P.wrep[(size_t)w * P.C + x.c] = value;
+  if (PXS_REPLY_STORE) P.wrep[(size_t)w * P.C + x.c] = value;
   const uint32_t issued = x.l_wiss[wi];
   if (P.max_requests == 0 || issued < P.max_requests) {
     const uint64_t nc = 1ull + w + (uint64_t)P.WK * issued;

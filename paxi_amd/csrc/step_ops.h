@@ -23,7 +23,7 @@ struct StepOps {
 // defined in k_paxos*.hip, k_abd.hip, k_wpaxos.hip; nullptr launch = not built
 StepOps paxos_step_ops(uint32_t N);
 StepOps abd_step_ops(uint32_t N);
-StepOps wpaxos_step_ops(uint32_t N);
+StepOps wpaxos_step_ops(uint32_t N, bool lds);   // lds: instance scalars in the tile image (Params::wlds)
 StepOps epaxos_step_ops(uint32_t N);
 
 #ifdef PXS_STEP_INSTANCE   // included by a kernel translation unit

@@ -38,11 +38,26 @@ __device__ __forceinline__ size_t wp_slot(const Params& P, const Rep<NT>& x, uin
   return (((size_t)x.blk * P.keys + key) * nrep<NT>(P) + x.r) * LANES + x.lane;
 }
 
-// bind the kpaxos of `key`: its registers from HBM, its window and pending list
-template <int NT>
+// bind the kpaxos of `key`: its registers, its window and pending list.  The
+// scalars come from LDS (LDS: the tile image holds them, wlds) or from the HBM
+// table; the digest, which only exec() reads, from HBM either way.
+template <int NT, bool LDS>
 __device__ __forceinline__ void wp_bind(const Params& P, Rep<NT>& x, uint32_t key) {
   const size_t si = wp_slot<NT>(P, x, key);
-  const uint4 a = P.wst[2 * si], b = P.wst[2 * si + 1];
+  uint4 a, b;
+  if constexpr (LDS) {
+    const uint32_t* w = x.l_inst + (((key * nrep<NT>(P) + x.r) * WP_WORDS) << 6) + x.lane;
+    a = make_uint4(w[0], w[64], w[128], w[192]);
+    b.w = w[256];
+    const uint64_t d = P.wdig[si];
+    b.x = (a.w >> 4) & 0x3Fu;
+    a.w &= 0xFFFF000Fu;
+    b.y = (uint32_t)d;
+    b.z = (uint32_t)(d >> 32);
+  } else {
+    a = P.wst[2 * si];
+    b = P.wst[2 * si + 1];
+  }
   x.key = key;
   x.ktag = key << 16;
   x.inst = key * nrep<NT>(P) + x.r;
@@ -65,12 +80,22 @@ __device__ __forceinline__ void wp_bind(const Params& P, Rep<NT>& x, uint32_t ke
   x.pend = P.wpend + si * PMAX;
   x.ci = ~0u;                        // the entry cache belongs to the bound window
 }
-template <int NT>
+template <int NT, bool LDS>
 __device__ __forceinline__ void wp_unbind(const Params& P, const Rep<NT>& x) {
   const size_t si = wp_slot<NT>(P, x, x.key);
-  P.wst[2 * si] = make_uint4(x.ballot, (uint32_t)x.slot, (uint32_t)x.execute,
-                             (x.active & 1u) | (x.exists << 1) | (x.iflags << 2) | (x.p1mask << 16));
-  P.wst[2 * si + 1] = make_uint4(x.npend, (uint32_t)x.digest, (uint32_t)(x.digest >> 32), x.pol | (x.cmask << 16));
+  const uint32_t meta = (x.active & 1u) | (x.exists << 1) | (x.iflags << 2) | (x.p1mask << 16);
+  if constexpr (LDS) {
+    uint32_t* w = x.l_inst + (((x.key * nrep<NT>(P) + x.r) * WP_WORDS) << 6) + x.lane;
+    w[0] = x.ballot;
+    w[64] = (uint32_t)x.slot;
+    w[128] = (uint32_t)x.execute;
+    w[192] = meta | (x.npend << 4);
+    w[256] = x.pol | (x.cmask << 16);
+    P.wdig[si] = x.digest;
+  } else {
+    P.wst[2 * si] = make_uint4(x.ballot, (uint32_t)x.slot, (uint32_t)x.execute, meta);
+    P.wst[2 * si + 1] = make_uint4(x.npend, (uint32_t)x.digest, (uint32_t)(x.digest >> 32), x.pol | (x.cmask << 16));
+  }
 }
 
 // r.paxi[m.Key] without a prior init: a nil *kpaxos, whose use panics in Go
@@ -213,10 +238,13 @@ __device__ __forceinline__ void wp_handle_request(const Params& P, Rep<NT>& x, u
   }
 }
 
-struct WPaxosProto {
+// LDS: the instance scalars live in the tile's LDS image (wlds); else in HBM
+template <bool LDS>
+struct WPaxosProtoT {
   static constexpr uint32_t kind = PAXISIM_WPAXOS;
   template <int NT>
   __device__ static __forceinline__ void load(const Params& P, Rep<NT>& x) {
+    x.l_inst = x.l_a;                // image region a: the instance scalars (LDS layout)
     x.nfwd = P.nfwd[rc(P, x.r, x.c)];
     x.e0 = 0;                        // entry of slot s: word 4*(s & (W-1)) of the lane's window
     x.es = 4;
@@ -231,9 +259,9 @@ struct WPaxosProto {
   template <int NT>
   __device__ static __forceinline__ void client_request(const Params& P, Rep<NT>& x, uint32_t cid) {
     PXS_CASE_T0
-    wp_bind<NT>(P, x, wl_key(P, x.kc, cid));
+    wp_bind<NT, LDS>(P, x, wl_key(P, x.kc, cid));
     wp_handle_request<NT>(P, x, mkreq(cid, PAXISIM_CLIENT_SRC));
-    wp_unbind<NT>(P, x);
+    wp_unbind<NT, LDS>(P, x);
     PXS_CASE_T1(0)
   }
   // registrations replica.go:25-32
@@ -250,7 +278,7 @@ struct WPaxosProto {
     }
     {
       PXS_CASE_T0
-      wp_bind<NT>(P, x, type == PAXISIM_MSG_REQUEST ? wl_key(P, x.kc, m.w) : hdr_key(m.x));
+      wp_bind<NT, LDS>(P, x, type == PAXISIM_MSG_REQUEST ? wl_key(P, x.kc, m.w) : hdr_key(m.x));
       // the entry of the message's slot (P2a / P2b / P3; harmless for the
       // others: any slot indexes the window): its load goes out with the bind's
       ecache<NT>(x, (m.z & (P.W - 1u)) * 4u);
@@ -311,10 +339,13 @@ struct WPaxosProto {
     }
     {
       PXS_CASE_T0
-      if (!clean) wp_unbind<NT>(P, x);
+      if (!clean) wp_unbind<NT, LDS>(P, x);
       PXS_CASE_T1(15)
     }
   }
 };
+
+using WPaxosProto = WPaxosProtoT<false>;
+using WPaxosProtoL = WPaxosProtoT<true>;
 
 }  // namespace pxs

@@ -8,7 +8,7 @@ OBJ=$R/build/var_$(basename "$OUT" .so)
 mkdir -p "$OBJ" "$(dirname "$R/$OUT")"
 cd "$R"
 SRCS=$(python3 -c "import __graft_entry__ as g; print(' '.join(g.HIP_SOURCES))")
-FLAGS=$(python3 -c "import __graft_entry__ as g; print(' '.join(g.HIP_FLAGS))")
+FLAGS=${BASEFLAGS:-$(python3 -c "import __graft_entry__ as g; print(' '.join(g.HIP_FLAGS))")}
 pids=()
 for s in $SRCS; do
   /opt/rocm/bin/hipcc $FLAGS "$@" -c -o "$OBJ/${s%.hip}.o" "paxi_amd/csrc/$s" &
