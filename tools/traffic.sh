@@ -15,6 +15,6 @@ cd /tmp
 i=0
 for ctr in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -d "$OUT/p$i" -o run --output-format csv -- python "$R/bench.py" --no-cpu-baseline --config "$CFG" "$@" > "$OUT/p$i.log" 2>&1 || { echo "pass $ctr failed rc=$?"; tail -5 "$OUT/p$i.log"; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -d "$OUT/p$i" -o run --output-format csv -- python "$R/bench.py" --no-cpu-baseline --no-shard-check --config "$CFG" "$@" > "$OUT/p$i.log" 2>&1 || { echo "pass $ctr failed rc=$?"; tail -5 "$OUT/p$i.log"; exit 1; }
 done
 python3 "$R/tools/traffic_summary.py" "$CFG" "$OUT" "$@" > "$R/gpurun_out/traffic/traffic_config$CFG.json" && cat "$R/gpurun_out/traffic/traffic_config$CFG.json"
