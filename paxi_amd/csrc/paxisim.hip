@@ -658,6 +658,14 @@ static Image proto_image(uint32_t protocol, uint32_t N, uint32_t W, uint32_t K, 
   return image_layout(logb, logb, logb, N, WK, D);
 }
 
+// The serial kernel (one wave per tile plays every replica, sim_core.h
+// sim_serial) for the protocols that have it; PAXISIM_SERIAL=0/1 overrides (A/B).
+static bool serial_for(uint32_t protocol) {
+  const char* e = getenv("PAXISIM_SERIAL");
+  (void)protocol;
+  return !e || atoi(e) != 0;
+}
+
 static int check_config(const paxisim_config* cfg, const paxisim_workload* wl, const paxisim_fault_process* fp,
                         uint32_t* N_out) {
   uint32_t N = 0;
@@ -700,7 +708,8 @@ static int check_config(const paxisim_config* cfg, const paxisim_workload* wl, c
   if (fp->slow_ppm && (fp->slow_min > fp->slow_max || fp->slow_max > cfg->max_delay))
     return fail(PAXISIM_EINVAL, "slow delay range exceeds max_delay");
   const Image img = proto_image(cfg->protocol, N, cfg->window, cfg->keys, wl->outstanding, cfg->max_delay + 2u, 0);
-  if (img.bytes > LDS_MAX)
+  // the serial kernel keeps only the image's tail (client tables on) in LDS
+  if ((serial_for(cfg->protocol) ? img.bytes - img.off_wcur + 2u * N * LANES : img.bytes) > LDS_MAX)
     return fail(PAXISIM_EUNSUPP, "workgroup image %u B exceeds LDS (%u B): reduce window/max_delay/replicas",
                 img.bytes, LDS_MAX);
   *N_out = N;
@@ -742,7 +751,13 @@ extern "C" int paxisim_destroy(paxisim* h) {
   return 0;
 }
 
-static StepOps step_ops_for(uint32_t protocol, uint32_t N, bool wlds) {
+static StepOps step_ops_for(uint32_t protocol, uint32_t N, bool wlds, bool serial) {
+  if (serial) {
+    if (protocol == PAXISIM_WPAXOS) return wpaxos_serial_step_ops(N, wlds);
+    if (protocol == PAXISIM_ABD) return abd_serial_step_ops(N);
+    if (protocol == PAXISIM_EPAXOS) return epaxos_serial_step_ops(N);
+    return paxos_serial_step_ops(N);
+  }
   if (protocol == PAXISIM_WPAXOS) return wpaxos_step_ops(N, wlds);
   if (protocol == PAXISIM_ABD) return abd_step_ops(N);
   if (protocol == PAXISIM_EPAXOS) return epaxos_step_ops(N);
@@ -869,7 +884,9 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
   if (P.protocol == PAXISIM_WPAXOS) {
     const char* ev = getenv("PAXISIM_WLDS");
     const uint32_t agn = P.AR ? (2u * N * LANES + 15u) & ~15u : 0u;
-    P.wlds = !(ev && atoi(ev) == 0) && proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D, 1).bytes + agn <= LDS_MAX;
+    // (the serial kernel keeps that image region in HBM: it need not fit)
+    P.wlds = !(ev && atoi(ev) == 0) &&
+             (serial_for(P.protocol) || proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D, 1).bytes + agn <= LDS_MAX);
   }
   P.img = proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D, P.wlds);
   {
@@ -877,7 +894,8 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     // the step kernel's registers leave wave slots for on every SIMD
     // (ceil(G*N/4) <= waves per SIMD) and the LDS holds, at most 4.
     int vgprs = 0, maxthr = 0;
-    h->ops = step_ops_for(P.protocol, N, P.wlds != 0);
+    const bool serial = serial_for(P.protocol);
+    h->ops = step_ops_for(P.protocol, N, P.wlds != 0, serial);
     if (h->ops.attrs(&vgprs, &maxthr) != hipSuccess || vgprs <= 0) vgprs = 512;
     if (maxthr <= 0) maxthr = (int)(N * LANES);
     const uint32_t alloc = ((uint32_t)vgprs + 7u) / 8u * 8u;
@@ -900,6 +918,11 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     P.off_agn = P.img.bytes;
     P.off_stage = base;
     P.lds_bytes = base + P.J * N * LANES * 16u;
+    if (serial) {   // one tile per workgroup; LDS: the image tail and the arrival counts
+      P.G = 1;
+      P.J = 0;
+      P.lds_bytes = base - P.img.off_wcur;
+    }
   }
   P.C = (cfg->clusters + LANES * P.G - 1) / (LANES * P.G) * (LANES * P.G);
   const size_t C = P.C, NC = (size_t)N * C, NIC = (size_t)P.NI * C, blocks = C / LANES;

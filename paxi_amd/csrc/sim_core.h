@@ -1000,4 +1000,134 @@ __global__ void __launch_bounds__(max_threads<NT>(), min_waves<NT>()) sim_steps(
   }
 }
 
+// ---------------------------------------------------------------------------
+// The serial step kernel: one wave per 64-cluster tile plays
+// every replica of its clusters in turn, replica 0 to N-1, each step.  A
+// replica's sends land in buckets of later steps only (§3.3), so running the
+// replicas of a step one after another is the same step as running them side
+// by side - it is how the oracle runs them.  No wave waits at a step barrier
+// for the tile's busiest replica, and a wave needs only the mailbox counts and
+// client tables in LDS (the log windows and the other image regions stay in
+// the HBM image), so many more tiles are resident per CU.  The replica's
+// registers are loaded from and stored to HBM around each replica-step.
+// ---------------------------------------------------------------------------
+#ifndef PXS_SERIAL_WAVES
+#define PXS_SERIAL_WAVES 2   // waves per SIMD the register budget must allow (2: <= 256 VGPRs; A/B r3: 3 waves at 168 VGPRs spill 127 and run 10-24% slower)
+#endif
+template <int NT>
+__device__ __forceinline__ void rep_counters_zero(Rep<NT>& x) {
+#pragma unroll
+  for (uint32_t k = 0; k < PAXISIM_NMSG / 2; k++) x.dvp[k] = 0;
+  x.client = x.sent = x.dropped = x.discarded = x.commits = x.replies = 0;
+}
+template <int NT>
+__device__ __forceinline__ void rep_counters_flush(const Params& P, const Rep<NT>& x) {
+  const uint32_t r = x.r;
+  const uint64_t c = x.c;
+#pragma unroll
+  for (uint32_t k = 1; k < PAXISIM_NMSG; k++)
+    if (dv_get(x, k)) P.stats[krc(P, ST_DELIV0 + k, r, c)] += dv_get(x, k);
+  if (x.client) P.stats[krc(P, ST_CLIENT, r, c)] += x.client;
+  if (x.sent) P.stats[krc(P, ST_SENT, r, c)] += x.sent;
+  if (x.dropped) P.stats[krc(P, ST_DROPPED, r, c)] += x.dropped;
+  if (x.discarded) P.stats[krc(P, ST_DISCARDED, r, c)] += x.discarded;
+  if (x.commits) P.stats[krc(P, ST_COMMITS, r, c)] += x.commits;
+  if (x.replies) P.stats[krc(P, ST_REPLIES, r, c)] += x.replies;
+}
+
+#ifndef PXS_SERIAL_WAVES_ABD
+#define PXS_SERIAL_WAVES_ABD 3   // ABD's kernels fit 168 VGPRs without spilling
+#endif
+template <class Proto> constexpr int serial_waves() {
+  return Proto::kind == PAXISIM_ABD ? PXS_SERIAL_WAVES_ABD : PXS_SERIAL_WAVES;
+}
+template <int NT, class Proto>
+__global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Params P, uint32_t t0, uint32_t nsteps) {
+  extern __shared__ uint4 lds[];
+  const uint32_t bound = __builtin_amdgcn_readfirstlane(*P.bound);
+  const uint32_t blk = blockIdx.x;
+  if ((uint64_t)blk * LANES >= bound) return;
+  const uint32_t N = nrep<NT>(P);
+  uint8_t* img = P.image + (size_t)blk * P.img.bytes;
+  // LDS holds the image from the client tables on: [off_wcur, bytes), then the arrival counts
+  const uint32_t tail = P.img.off_wcur;
+  {
+    const uint32_t nb = (P.img.bytes - tail) / 16u;
+    const uint4* g = reinterpret_cast<const uint4*>(img + tail);
+    for (uint32_t k = threadIdx.x; k < nb; k += LANES) lds[k] = g[k];
+  }
+  uint8_t* L = reinterpret_cast<uint8_t*>(lds);
+  Rep<NT> x;
+  x.lane = threadIdx.x;
+  x.blk = blk;
+  x.c = (uint64_t)blk * LANES + x.lane;
+  x.gid = P.cluster_base + P.cl_of[x.c];
+  x.l_wcur = reinterpret_cast<uint32_t*>(L + (P.img.off_wcur - tail));
+  x.l_wiss = reinterpret_cast<uint32_t*>(L + (P.img.off_wiss - tail));
+  x.l_poison = reinterpret_cast<uint32_t*>(L + (P.img.off_poison - tail));
+  x.l_cnt = L + (P.img.off_cnt - tail);
+  x.l_agn = L + (P.off_agn - tail);
+  x.rec = P.rec + (size_t)blk * P.rec_per_block;
+  if (P.AR)
+    for (uint32_t k = x.lane; k < 2u * N * LANES; k += LANES) x.l_agn[k] = 0;
+  const bool live = x.c < bound;
+  x.es = Proto::kind == PAXISIM_WPAXOS ? 4u : LANES;
+  x.kc = live ? P.kc[x.c] : 0u;
+  uint32_t b0 = t0 % P.D;
+  for (uint32_t t = t0; t < t0 + nsteps; t++) {
+    if (live && x.l_poison[x.lane] >= t) {
+#pragma nounroll
+      for (uint32_t r = 0; r < N; r++) {
+        x.r = r;
+        x.t = t;
+        x.b0 = b0;
+        x.ci = ~0u;
+        // HBM-resident image regions (a WPaxos bind repoints these at its window)
+        x.l_a = reinterpret_cast<uint32_t*>(img + P.img.off_a);
+        x.l_b = reinterpret_cast<uint32_t*>(img + P.img.off_b);
+        x.l_c = reinterpret_cast<uint32_t*>(img + P.img.off_c);
+        const size_t i = rc(P, r, x.c);
+        x.flags = P.flags[i];
+        x.kvver = P.kv ? P.kv_ver[i] : 0u;
+        Proto::template load<NT>(P, x);
+        rep_counters_zero<NT>(x);
+#ifdef PXS_STAMPS
+        Stamps st = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        const unsigned long long sr0 = stamp();
+        replica_step<NT, Proto, false>(P, x, &st);
+        st.steps = 1;
+        st.barrier = stamp() - sr0;   // serial kernel: the whole replica-step (no barrier)
+        if (x.lane == 0 && P.dbg) {
+          unsigned long long* d = &P.dbg[((size_t)blk * 16 + r) * DBG_PER];
+          atomicAdd(&d[0], st.setup); atomicAdd(&d[1], st.loop); atomicAdd(&d[2], st.barrier);
+          atomicAdd(&d[3], st.trips); atomicAdd(&d[4], st.msgs); atomicAdd(&d[5], st.steps);
+          atomicAdd(&d[6], st.pick); atomicAdd(&d[7], st.disp);
+          atomicAdd(&d[8], st.wait); atomicAdd(&d[9], st.flush);
+          atomicAdd(&d[10], st.stage); atomicAdd(&d[11], st.tail);
+        }
+#else
+        replica_step<NT, Proto, false>(P, x);
+#endif
+        P.flags[i] = x.flags;
+        if (P.kv) P.kv_ver[i] = x.kvver;
+        Proto::template store<NT>(P, x);
+        rep_counters_flush<NT>(P, x);
+      }
+    }
+    if (P.AR && live) agree_drain<NT>(P, x, t & 1u);   // this step's arrivals, replica order
+    if (++b0 == P.D) b0 = 0;
+  }
+  if (P.compact && live) {
+    uint32_t any = 0;
+    const uint32_t nbox = P.D * N * (N + 1u);
+    for (uint32_t b = 0; b < nbox; b++) any |= x.l_cnt[(b << 6) | x.lane];
+    P.qf[x.c] = any ? 0u : 1u;
+  }
+  {
+    const uint32_t nb = (P.img.bytes - tail) / 16u;
+    uint4* g = reinterpret_cast<uint4*>(img + tail);
+    for (uint32_t k = threadIdx.x; k < nb; k += LANES) g[k] = lds[k];
+  }
+}
+
 }  // namespace pxs

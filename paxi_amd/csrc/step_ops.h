@@ -18,9 +18,15 @@ struct StepOps {
   hipError_t (*occupancy)(const Params& P, int* blocks);
   hipError_t (*attrs)(int* vgprs, int* max_threads);
   bool staged;   // the instance carries the LDS-staged merge loop (sim_core.h stage_built)
+  bool serial;   // the serial kernel: one wave per tile plays every replica (sim_core.h sim_serial)
 };
 
 // defined in k_paxos*.hip, k_abd.hip, k_wpaxos.hip; nullptr launch = not built
+// *_serial_step_ops: the serial kernel of the same protocol and N
+StepOps paxos_serial_step_ops(uint32_t N);
+StepOps abd_serial_step_ops(uint32_t N);
+StepOps wpaxos_serial_step_ops(uint32_t N, bool lds);
+StepOps epaxos_serial_step_ops(uint32_t N);
 StepOps paxos_step_ops(uint32_t N);
 StepOps abd_step_ops(uint32_t N);
 StepOps wpaxos_step_ops(uint32_t N, bool lds);   // lds: instance scalars in the tile image (Params::wlds)
@@ -55,6 +61,34 @@ struct StepInstance {
     return e;
   }
   static StepOps ops() { return StepOps{&launch, &set_lds, &occupancy, &attrs, stage_built<NT, Proto>()}; }
+};
+
+// The serial kernel (sim_core.h sim_serial): one wave per tile, P.G = 1,
+// P.lds_bytes of LDS per workgroup.
+template <int NT, class Proto>
+struct SerialInstance {
+  static hipError_t launch(const Params& P, hipStream_t s, uint32_t t0, uint32_t n) {
+    sim_serial<NT, Proto><<<(unsigned)(P.C / LANES), LANES, (size_t)P.lds_bytes, s>>>(P, t0, n);
+    return hipGetLastError();
+  }
+  static hipError_t set_lds(int bytes) {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&sim_serial<NT, Proto>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  }
+  static hipError_t occupancy(const Params& P, int* blocks) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, reinterpret_cast<const void*>(&sim_serial<NT, Proto>),
+                                                        (int)LANES, (size_t)P.lds_bytes);
+  }
+  static hipError_t attrs(int* v, int* maxthr) {
+    hipFuncAttributes a;
+    hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&sim_serial<NT, Proto>));
+    if (e == hipSuccess) {
+      *v = a.numRegs;
+      *maxthr = a.maxThreadsPerBlock;
+    }
+    return e;
+  }
+  static StepOps ops() { return StepOps{&launch, &set_lds, &occupancy, &attrs, false, true}; }
 };
 #endif
 

@@ -147,10 +147,20 @@ def test_single_cluster_and_ragged_tail():
 
 
 def test_oversized_workgroup_image_is_refused():
-    """N=9 with a 64-slot window needs more than 160 KB of LDS: EUNSUPP, not a crash."""
+    """16 replicas with 15-step delays need 174 KB of mailbox counts in LDS: EUNSUPP, not a crash."""
     from paxi_amd.sim import PaxisimError
     with pytest.raises(PaxisimError, match="exceeds LDS"):
-        _sim()(abi.make_config(npz=[3, 3, 3], clusters=64, window=64), abi.make_workload())
+        _sim()(abi.make_config(npz=[16], clusters=64, max_delay=14), abi.make_workload())
+
+
+def test_window64_n9():
+    """N=9 with SURVEY 8's 64-slot window: the serial kernel keeps the windows in
+    HBM (the replica-per-wave kernel's 160 KB of LDS could not hold them)."""
+    cfg = abi.make_config(npz=[3, 3, 3], clusters=130, seed=6, window=64, q1=abi.Q_FGRID_Q1, q2=abi.Q_FGRID_Q2, fz=1)
+    wl = abi.make_workload(outstanding=8, target=0)
+    fp = abi.make_fault_process(drop_ppm=3000, drop_len=25, slow_ppm=3000, slow_len=25, slow_min=1, slow_max=4)
+    g, o = run_both(cfg, wl, fp, steps=300)
+    assert_same(g, o, "N=9 W=64")
 
 
 def test_window32_n5():

@@ -1,0 +1,27 @@
+#!/bin/bash
+# Build a variant of libpaxisim.so that recompiles only some translation units
+# with extra flags and links the default build's objects for the rest (A/B of
+# one kernel instance without a full rebuild).  Run `python __graft_entry__.py` first.
+# Usage: tools/build_variant_tu.sh <out.so> "<k_x.hip k_y.hip>" [-DFLAG=V ...]
+set -e -o pipefail
+OUT=$1; TUS=$2; shift 2
+R=$(cd "$(dirname "$0")/.." && pwd)
+OBJ=$R/build/var_$(basename "$OUT" .so)
+mkdir -p "$OBJ" "$(dirname "$R/$OUT")"
+cd "$R"
+FLAGS=$(python3 -c "import __graft_entry__ as g; print(' '.join(g.HIP_FLAGS))")
+SRCS=$(python3 -c "import __graft_entry__ as g; print(' '.join(g.HIP_SOURCES))")
+objs=()
+pids=()
+for s in $SRCS; do
+  if [[ " $TUS " == *" $s "* ]]; then
+    /opt/rocm/bin/hipcc $FLAGS "$@" -c -o "$OBJ/${s%.hip}.o" "paxi_amd/csrc/$s" &
+    pids+=($!)
+    objs+=("$OBJ/${s%.hip}.o")
+  else
+    objs+=("build/hip/${s%.hip}.o")
+  fi
+done
+for p in "${pids[@]}"; do wait "$p"; done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$R/$OUT" "${objs[@]}" -ldl
+echo "built $OUT"
