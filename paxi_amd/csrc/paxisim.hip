@@ -921,7 +921,8 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     if (serial) {   // one tile per workgroup; LDS: the image tail and the arrival counts
       P.G = 1;
       P.J = 0;
-      P.lds_bytes = base - P.img.off_wcur;
+      P.lds_tail = PXS_CLIENT_LDS ? P.img.off_wcur : P.img.off_poison;
+      P.lds_bytes = base - P.lds_tail;
     }
   }
   P.C = (cfg->clusters + LANES * P.G - 1) / (LANES * P.G) * (LANES * P.G);

@@ -124,6 +124,7 @@ struct Params {
   Image img;
   uint32_t J, off_stage;   // LDS stage: J staged picks per replica at LDS byte off_stage ([r][J][64] x 16 B)
   uint32_t lds_bytes;      // LDS per cluster group (16-B multiple): the image + the stage
+  uint32_t lds_tail;       // serial kernel: the image bytes [lds_tail, bytes) are staged in LDS (PXS_CLIENT_LDS)
   uint32_t G;              // cluster groups (64-cluster tiles) per workgroup
   uint32_t rec_per_block;  // D*N*NS*M*64
   const DevFault* faults;
@@ -369,6 +370,12 @@ __device__ __forceinline__ void stamp_case(const Params& P, uint32_t blk, uint32
 #else
 #define PXS_CASE_T0
 #define PXS_CASE_T1(k)
+#endif
+
+// The serial kernel keeps the client tables (wcur / wiss) in the HBM image
+// (0) or stages them into LDS with the mailbox counts (1, A/B).
+#ifndef PXS_CLIENT_LDS
+#define PXS_CLIENT_LDS 1   // (A/B r3: the HBM tables cost config 2 6%, configs 4 and 5 4%)
 #endif
 
 // ---- SoA addressing --------------------------------------------------------

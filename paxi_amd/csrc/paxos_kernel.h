@@ -286,6 +286,9 @@ __device__ __forceinline__ void ghost_p2b(const Params& P, Rep<NT>& x, int32_t m
   }
 }
 
+#ifndef PXS_P2B_EAGER
+#define PXS_P2B_EAGER 0   // 1: HandleP2b reads the entry's ack word with its ballot and flags (A/B)
+#endif
 template <int NT>
 __device__ __forceinline__ bool in_window(const Params& P, const Rep<NT>& x, int32_t s) {
   return s >= x.execute && s < x.execute + (int32_t)P.W;
@@ -530,6 +533,7 @@ __device__ __forceinline__ void paxos_handle_p2b(const Params& P, Rep<NT>& x, ui
   const uint32_t i = eidx<NT>(P, x, ms);
   const uint32_t c = eb(x, i);
   const uint32_t eb0 = ea(x, i);
+  const uint32_t ea0 = PXS_P2B_EAGER ? ec(x, i) : 0u;   // (HBM window: the three words in one round trip)
   if (!(c & EF_EXISTS) || mb < eb0 || (c & EF_COMMIT)) return;
   if (mb > x.ballot) {
     x.ballot = mb;
@@ -541,7 +545,7 @@ __device__ __forceinline__ void paxos_handle_p2b(const Params& P, Rep<NT>& x, ui
       x.stop = true;
       return;
     }
-    const uint32_t ack = ec(x, i) | (1u << src);
+    const uint32_t ack = (PXS_P2B_EAGER ? ea0 : ec(x, i)) | (1u << src);
     set_c(x, i, ack);
     if (quorum_ok(P, P.q2, ack)) {
       set_b(x, i, c | EF_COMMIT);
@@ -607,10 +611,11 @@ __device__ __forceinline__ bool p2b_absorb(const Params& P, Rep<NT>& x, uint32_t
   const uint32_t i = eidx<NT>(P, x, ms);
   const uint32_t c = eb(x, i);
   const uint32_t eb0 = ea(x, i);
+  const uint32_t ea0 = PXS_P2B_EAGER ? ec(x, i) : 0u;
   if (!(c & EF_EXISTS) || mb < eb0 || (c & EF_COMMIT)) return true;
   if (bal_id(mb) == x.r && mb == eb0) {
     if (!(c & EF_QUORUM)) return false;                 // nil quorum: the full handler poisons
-    const uint32_t ack = ec(x, i) | (1u << src);
+    const uint32_t ack = (PXS_P2B_EAGER ? ea0 : ec(x, i)) | (1u << src);
     if (quorum_ok(P, P.q2, ack)) return false;          // commit: the full handler
     set_c(x, i, ack);
   }

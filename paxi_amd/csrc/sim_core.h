@@ -1020,19 +1020,28 @@ __device__ __forceinline__ void rep_counters_zero(Rep<NT>& x) {
   for (uint32_t k = 0; k < PAXISIM_NMSG / 2; k++) x.dvp[k] = 0;
   x.client = x.sent = x.dropped = x.discarded = x.commits = x.replies = 0;
 }
+// PXS_COUNTER_ATOMIC: the per-replica-step counts go out as fire-and-forget
+// atomic adds (no load to wait for) instead of read-modify-writes
+#ifndef PXS_COUNTER_ATOMIC
+#define PXS_COUNTER_ATOMIC 1   // (A/B r3, config 2: +4.9%)
+#endif
+__device__ __forceinline__ void stat_add(uint32_t* p, uint32_t v) {
+  if (PXS_COUNTER_ATOMIC) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p += v;
+}
 template <int NT>
 __device__ __forceinline__ void rep_counters_flush(const Params& P, const Rep<NT>& x) {
   const uint32_t r = x.r;
   const uint64_t c = x.c;
 #pragma unroll
   for (uint32_t k = 1; k < PAXISIM_NMSG; k++)
-    if (dv_get(x, k)) P.stats[krc(P, ST_DELIV0 + k, r, c)] += dv_get(x, k);
-  if (x.client) P.stats[krc(P, ST_CLIENT, r, c)] += x.client;
-  if (x.sent) P.stats[krc(P, ST_SENT, r, c)] += x.sent;
-  if (x.dropped) P.stats[krc(P, ST_DROPPED, r, c)] += x.dropped;
-  if (x.discarded) P.stats[krc(P, ST_DISCARDED, r, c)] += x.discarded;
-  if (x.commits) P.stats[krc(P, ST_COMMITS, r, c)] += x.commits;
-  if (x.replies) P.stats[krc(P, ST_REPLIES, r, c)] += x.replies;
+    if (dv_get(x, k)) stat_add(&P.stats[krc(P, ST_DELIV0 + k, r, c)], dv_get(x, k));
+  if (x.client) stat_add(&P.stats[krc(P, ST_CLIENT, r, c)], x.client);
+  if (x.sent) stat_add(&P.stats[krc(P, ST_SENT, r, c)], x.sent);
+  if (x.dropped) stat_add(&P.stats[krc(P, ST_DROPPED, r, c)], x.dropped);
+  if (x.discarded) stat_add(&P.stats[krc(P, ST_DISCARDED, r, c)], x.discarded);
+  if (x.commits) stat_add(&P.stats[krc(P, ST_COMMITS, r, c)], x.commits);
+  if (x.replies) stat_add(&P.stats[krc(P, ST_REPLIES, r, c)], x.replies);
 }
 
 #ifndef PXS_SERIAL_WAVES_ABD
@@ -1049,8 +1058,9 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
   if ((uint64_t)blk * LANES >= bound) return;
   const uint32_t N = nrep<NT>(P);
   uint8_t* img = P.image + (size_t)blk * P.img.bytes;
-  // LDS holds the image from the client tables on: [off_wcur, bytes), then the arrival counts
-  const uint32_t tail = P.img.off_wcur;
+  // LDS holds the image tail [tail, bytes) - from the client tables on, or
+  // (P.lds_tail = off_poison) from the poison steps on - then the arrival counts
+  const uint32_t tail = P.lds_tail;
   {
     const uint32_t nb = (P.img.bytes - tail) / 16u;
     const uint4* g = reinterpret_cast<const uint4*>(img + tail);
@@ -1062,8 +1072,13 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
   x.blk = blk;
   x.c = (uint64_t)blk * LANES + x.lane;
   x.gid = P.cluster_base + P.cl_of[x.c];
-  x.l_wcur = reinterpret_cast<uint32_t*>(L + (P.img.off_wcur - tail));
-  x.l_wiss = reinterpret_cast<uint32_t*>(L + (P.img.off_wiss - tail));
+  if (PXS_CLIENT_LDS) {
+    x.l_wcur = reinterpret_cast<uint32_t*>(L + (P.img.off_wcur - tail));
+    x.l_wiss = reinterpret_cast<uint32_t*>(L + (P.img.off_wiss - tail));
+  } else {                                                   // client tables in the HBM image
+    x.l_wcur = reinterpret_cast<uint32_t*>(img + P.img.off_wcur);
+    x.l_wiss = reinterpret_cast<uint32_t*>(img + P.img.off_wiss);
+  }
   x.l_poison = reinterpret_cast<uint32_t*>(L + (P.img.off_poison - tail));
   x.l_cnt = L + (P.img.off_cnt - tail);
   x.l_agn = L + (P.off_agn - tail);

@@ -9,7 +9,7 @@ import csv
 import json
 import sys
 
-rows = [r for r in csv.DictReader(open(sys.argv[1])) if "sim_steps" in r["Kernel_Name"]]
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if "sim_steps" in r["Kernel_Name"] or "sim_serial" in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 steps = int(sys.argv[2])
 if steps == 0:

@@ -16,7 +16,7 @@ import sys
 def per_dispatch(path, counter):
     agg = collections.defaultdict(float)
     for r in csv.DictReader(open(path)):
-        if "sim_steps" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+        if ("sim_steps" in r["Kernel_Name"] or "sim_serial" in r["Kernel_Name"]) and r["Counter_Name"] == counter:
             agg[int(r["Dispatch_Id"])] += float(r["Counter_Value"])
     return [agg[k] for k in sorted(agg)]
 
