@@ -188,8 +188,10 @@ __device__ void ep_execute(const Params& P, Rep<NT>& x) {
       if (e.status != EP_COMMITTED) break;
       x.digest = mix64(x.digest ^ (((uint64_t)((id << 24) | (uint32_t)sl) << 32) | e.cmd));
       x.execute++;                                       // Execute calls, re-executions included
-      const uint32_t v = P.kv && e.req ? kv_get<NT>(P, x, e.cmd) : 0u;   // v := r.Execute(i.cmd)
-      if (P.kv) kv_exec<NT>(P, x, e.cmd);
+      const uint32_t h = P.kv ? wl_hash(x.kc, e.cmd) : 0u;
+      const uint32_t key = P.kv ? kv_key<NT>(P, x, h, e.cmd) : 0u;
+      const uint32_t v = P.kv && e.req ? kv_get<NT>(P, x, key) : 0u;   // v := r.Execute(i.cmd)
+      if (P.kv) kv_exec<NT>(P, x, h, key, e.cmd);
       if (e.req) {
         ep_reply<NT>(P, x, e, v);
         P.ep_inst[ii] = make_uint4(e.cmd, e.req, e.acks | (e.nrep << 16), (uint32_t)e.seq);

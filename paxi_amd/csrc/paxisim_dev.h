@@ -367,9 +367,14 @@ __device__ __forceinline__ void stamp_case(const Params& P, uint32_t blk, uint32
 }
 #define PXS_CASE_T0 const uint32_t pxs_c0 = (uint32_t)stamp();
 #define PXS_CASE_T1(k) if constexpr (NT != 0) stamp_case(P, x.blk, x.r, (k), pxs_c0);   // (NT = 0: a spill codegen bug)
+// sub-handler regions (slots the Multi-Paxos kernels leave free: 5, 9-13)
+#define PXS_SUB_T0(v) const uint32_t v = (uint32_t)stamp();
+#define PXS_SUB_T1(v, k) if constexpr (NT != 0) stamp_case(P, x.blk, x.r, (k), v);
 #else
 #define PXS_CASE_T0
 #define PXS_CASE_T1(k)
+#define PXS_SUB_T0(v)
+#define PXS_SUB_T1(v, k)
 #endif
 
 // The serial kernel keeps the client tables (wcur / wiss) in the HBM image

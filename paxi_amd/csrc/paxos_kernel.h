@@ -366,37 +366,57 @@ __device__ __forceinline__ void handle_request(const Params& P, Rep<NT>& x, uint
 #ifndef PXS_REPLY_VALUE
 #define PXS_REPLY_VALUE 1   // 0: replies carry no value (A/B attribution only; not the reference's behaviour)
 #endif
+// (the key is computed once per executed command: kv_key)
 template <int NT>
-__device__ __forceinline__ uint32_t kv_get(const Params& P, Rep<NT>& x, uint32_t cmd) {
+__device__ __forceinline__ uint32_t kv_key(const Params& P, const Rep<NT>& x, uint32_t h, uint32_t cmd) {
+  // a per-key instance (HBM log: WPaxos, M2Paxos, KPaxos) only executes commands of its own key
+  return hbm_log(x) ? x.key : wl_key_h(P, h, cmd);
+}
+template <int NT>
+__device__ __forceinline__ uint32_t kv_get(const Params& P, Rep<NT>& x, uint32_t key) {
   if (!PXS_REPLY_VALUE) return 0u;
-  const uint32_t key = hbm_log(x) ? x.key : wl_key(P, x.kc, cmd);
   const uint32_t* a = &P.kv_val[((size_t)key * nrep<NT>(P) + x.r) * P.C + x.c];
   return PXS_KV_LDG ? ldg(a) : *a;
 }
 template <int NT>
-__device__ __forceinline__ void kv_exec(const Params& P, Rep<NT>& x, uint32_t cmd) {
-  if (!wl_write(P, x.kc, cmd)) return;
-  // a per-key instance (HBM log: WPaxos, M2Paxos, KPaxos) only executes commands of its own key
-  const uint32_t key = hbm_log(x) ? x.key : wl_key(P, x.kc, cmd);
+__device__ __forceinline__ void kv_exec(const Params& P, Rep<NT>& x, uint32_t h, uint32_t key, uint32_t cmd) {
+  if (!wl_write_h(P, h)) return;
   P.kv_val[((size_t)key * nrep<NT>(P) + x.r) * P.C + x.c] = cmd;
   x.kvver++;
 }
 
+// hi / hc: the entry index and flags the caller has just written, which exec
+// then does not read back.  With the window in HBM (three planes, the serial
+// kernel) each slot's iteration loads the next slot's flags before it issues
+// its own stores (PXS_EXEC_AHEAD), so the loop's exit test does not wait for
+// them (vmcnt retires loads and stores in issue order).
+#ifndef PXS_EXEC_AHEAD
+#define PXS_EXEC_AHEAD 1
+#endif
 template <int NT>
-__device__ __forceinline__ void paxos_exec(const Params& P, Rep<NT>& x) {     // paxos.go:345-369
+__device__ __forceinline__ void paxos_exec(const Params& P, Rep<NT>& x, uint32_t hi = ~0u,
+                                           uint32_t hc = 0u) {     // paxos.go:345-369
+  uint32_t ni = ~0u, nc = 0u;                                      // the next slot's entry, loaded ahead
   for (;;) {
     if (hbm_log(x)) {                                              // skip the HBM read of an uncommitted entry
       if (P.W <= 16u ? !((x.cmask >> ((uint32_t)x.execute & (P.W - 1u))) & 1u) : x.execute > x.slot) break;
     }
     const uint32_t i = eidx<NT>(P, x, x.execute);
-    const uint32_t c = eb(x, i);
+    const uint32_t c = i == hi ? hc : (i == ni ? nc : eb(x, i));
+    hi = ~0u;
     if ((c & (EF_EXISTS | EF_COMMIT)) != (EF_EXISTS | EF_COMMIT)) break;
+    if (PXS_EXEC_AHEAD && x.hw && !hbm_log(x)) {
+      ni = eidx<NT>(P, x, x.execute + 1);
+      nc = x.l_b[ni];
+    }
     if (x.iflags & PAXISIM_F_WOVF) x.flags |= PAXISIM_F_UNFAITHFUL;
     const uint32_t cmd = c & CMD_MASK;
+    const uint32_t h = P.kv ? wl_hash(x.kc, cmd) : 0u;
+    const uint32_t key = P.kv ? kv_key<NT>(P, x, h, cmd) : 0u;
     if (c & (EF_REQSELF | EF_REQEXT))                             // Reply{Value: p.Execute(cmd)}, paxos.go:352-362
-      request_reply<NT>(P, x, ereq<NT>(P, x, i, c), cmd, P.kv ? kv_get<NT>(P, x, cmd) : 0u);
+      request_reply<NT>(P, x, ereq<NT>(P, x, i, c), cmd, P.kv ? kv_get<NT>(P, x, key) : 0u);
     x.digest = mix64(x.digest ^ (((uint64_t)(uint32_t)x.execute << 32) | cmd));
-    if (P.kv) kv_exec<NT>(P, x, cmd);                              // p.Execute(e.command), paxos.go:352
+    if (P.kv) kv_exec<NT>(P, x, h, key, cmd);                      // p.Execute(e.command), paxos.go:352
     set_b(x, i, 0u);                                               // delete(p.log, execute)
     x.execute++;
     if ((uint32_t)x.execute % CKI == 0) {
@@ -530,11 +550,13 @@ __device__ __forceinline__ void paxos_handle_p2b(const Params& P, Rep<NT>& x, ui
     else if (x.iflags & PAXISIM_F_WOVF) x.flags |= PAXISIM_F_UNFAITHFUL;
     return;
   }
+  PXS_SUB_T0(pxs_e0)
   const uint32_t i = eidx<NT>(P, x, ms);
   const uint32_t c = eb(x, i);
   const uint32_t eb0 = ea(x, i);
   const uint32_t ea0 = PXS_P2B_EAGER ? ec(x, i) : 0u;   // (HBM window: the three words in one round trip)
   if (!(c & EF_EXISTS) || mb < eb0 || (c & EF_COMMIT)) return;
+  PXS_SUB_T1(pxs_e0, 10)
   if (mb > x.ballot) {
     x.ballot = mb;
     x.active = 0;
@@ -545,8 +567,10 @@ __device__ __forceinline__ void paxos_handle_p2b(const Params& P, Rep<NT>& x, ui
       x.stop = true;
       return;
     }
+    PXS_SUB_T0(pxs_a0)
     const uint32_t ack = (PXS_P2B_EAGER ? ea0 : ec(x, i)) | (1u << src);
     set_c(x, i, ack);
+    PXS_SUB_T1(pxs_a0, 11)
     if (quorum_ok(P, P.q2, ack)) {
       set_b(x, i, c | EF_COMMIT);
       x.commits++;
@@ -556,7 +580,9 @@ __device__ __forceinline__ void paxos_handle_p2b(const Params& P, Rep<NT>& x, ui
         if (!q) { x.flags |= PAXISIM_F_POISON; x.stop = true; return; }   // nil r.Reply
         request_reply<NT>(P, x, q, req_cid(q), 0u);   // Reply{Command}: no Value
       } else {
-        paxos_exec<NT>(P, x);
+        PXS_SUB_T0(pxs_x0)
+        paxos_exec<NT>(P, x, i, c | EF_COMMIT);
+        PXS_SUB_T1(pxs_x0, 9)
       }
     }
   }
@@ -588,6 +614,10 @@ __device__ __forceinline__ void paxos_handle_p3(const Params& P, Rep<NT>& x, uin
       }
       return;
     }
+    PXS_SUB_T0(pxs_x1)
+    paxos_exec<NT>(P, x, i, c);
+    PXS_SUB_T1(pxs_x1, 5)
+    return;
   } else if (ms < x.execute) {
     ghost_commit<NT>(P, x, ms);
   } else {

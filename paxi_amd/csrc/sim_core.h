@@ -34,6 +34,7 @@ struct Rep {
   uint4 ce;                             // HBM-resident window (es = 4): entry at word ci, cached (paxos_kernel.h)
   uint32_t ci;
   uint32_t cmask;                       // HBM-resident window: committed entries, one bit per window slot (W <= 16)
+  bool hw;                              // the log window is in HBM (a kernel constant: sim_serial)
   uint32_t* reqx;                       // request side table, indexed like the log
   uint32_t* pend;                       // pending request k at pend[k * pstride]
   uint32_t pstride;
@@ -310,8 +311,8 @@ __device__ __forceinline__ uint32_t mod_magic(uint32_t x, uint32_t d, uint32_t m
   uint32_t r = x - d * __umulhi(x, m);
   return r >= d ? r - d : r;
 }
-__device__ __forceinline__ uint32_t wl_key(const Params& P, uint32_t kc, uint32_t cid) {
-  const uint32_t h = wl_hash(kc, cid);
+// the key of command cid given h = wl_hash(kc, cid)
+__device__ __forceinline__ uint32_t wl_key_h(const Params& P, uint32_t h, uint32_t cid) {
   if (P.locality_ppm) {
     const uint32_t w = mod_magic(cid - 1u, P.WK, P.wk_magic);        // (cid-1) % WK
     const uint32_t z = P.wzone[w], nk = P.wnk[w];                    // zone_of[target[w]], its key count
@@ -330,8 +331,14 @@ __device__ __forceinline__ uint32_t wl_key(const Params& P, uint32_t kc, uint32_
     default: return mod_magic(h, P.keys, P.keys_magic);
   }
 }
+__device__ __forceinline__ uint32_t wl_key(const Params& P, uint32_t kc, uint32_t cid) {
+  return wl_key_h(P, wl_hash(kc, cid), cid);
+}
+__device__ __forceinline__ bool wl_write_h(const Params& P, uint32_t h) {
+  return ppm_hit(fmix32(h ^ 0x27D4EB2Fu), P.write_ppm);
+}
 __device__ __forceinline__ bool wl_write(const Params& P, uint32_t kc, uint32_t cid) {
-  return ppm_hit(fmix32(wl_hash(kc, cid) ^ 0x27D4EB2Fu), P.write_ppm);
+  return wl_write_h(P, wl_hash(kc, cid));
 }
 
 #ifndef PXS_REPLY_STORE
@@ -703,6 +710,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
 #if !PXS_FLUSH_LATE
     intent_flush<NT>(P, x);                             // one emit point for all lanes
 #endif
+    PXS_SUB_T0(pxs_ab0)
     if constexpr ((Proto::kind == PAXISIM_PAXOS && (PXS_ABSORB9 || NT != 9)) ||
                   (Proto::kind == PAXISIM_ABD && PXS_ABSORB_ABD)) {
       // Next messages whose handling is short and send-free (a P2b that does
@@ -734,13 +742,16 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
         }
       }
     }
+    if constexpr (Proto::kind == PAXISIM_PAXOS) { PXS_SUB_T1(pxs_ab0, 12) }
 #if PXS_FLUSH_LATE
     // The handler's pending send is emitted after the absorbed messages (they
     // send nothing, so every link still sees its records in handler order):
     // the record loads issued while absorbing then precede this flush's
     // stores, and waiting for them does not wait for the stores (vmcnt
     // retires loads and stores in issue order).
+    PXS_SUB_T0(pxs_fl0)
     intent_flush<NT>(P, x);
+    if constexpr (Proto::kind == PAXISIM_PAXOS) { PXS_SUB_T1(pxs_fl0, 13) }
 #endif
 #ifdef PXS_STAMPS
     fe = stamp();
@@ -905,6 +916,7 @@ __global__ void __launch_bounds__(max_threads<NT>(), min_waves<NT>()) sim_steps(
   const bool live = x.c < bound && x.r < N;
   // the log layout is a constant of the instance (paxos_kernel.h: hbm_log)
   x.es = Proto::kind == PAXISIM_WPAXOS ? 4u : LANES;
+  x.hw = Proto::kind == PAXISIM_WPAXOS;
   x.ci = ~0u;
   if (live) {
     const size_t i = rc(P, x.r, x.c);
@@ -1087,6 +1099,7 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
     for (uint32_t k = x.lane; k < 2u * N * LANES; k += LANES) x.l_agn[k] = 0;
   const bool live = x.c < bound;
   x.es = Proto::kind == PAXISIM_WPAXOS ? 4u : LANES;
+  x.hw = true;   // every window is in the HBM image here
   x.kc = live ? P.kc[x.c] : 0u;
   uint32_t b0 = t0 % P.D;
   for (uint32_t t = t0; t < t0 + nsteps; t++) {

@@ -52,6 +52,8 @@ for r in range(N):
           f" per step: stage {tot[10]/st:7.0f} after lane 0 done (other lanes trips) {tot[11]/st:7.0f}")
 NAMES = {0: "client req+bind", 1: "REQUEST", 2: "REPLY", 3: "P1A", 4: "P1B", 6: "P2A", 7: "P2B", 8: "P3",
          9: "GET", 10: "GETREPLY", 11: "SET", 12: "SETREPLY", 13: "LEADERCHG", 14: "bind", 15: "unbind"}
+if config in (2, 4):   # Multi-Paxos: sub-handler regions in the slots ABD / WPaxos use (paxisim_dev.h PXS_SUB_T*)
+    NAMES.update({5: " P3>exec", 9: " P2B>exec", 10: " P2B>entry", 11: " P2B>ack", 12: "absorb loop", 13: "send flush"})
 print("handler paths (cycles per wave-step, runs per wave-step, cycles per run), summed over replicas:")
 cyc = [0] * 16
 runs = [0] * 16
