@@ -387,6 +387,8 @@ def main():
         avg_launch_ms = kms / max(1, launches)
         achieved = alg_bytes(d) / max(1, launches) / (avg_launch_ms / 1e3) / 1e9   # rank 0's kernel, GB/s
         proto = {3: "AbdProto", 5: "WPaxosProto"}.get(args.config, "PaxosProto")
+        # the library's default step kernel is the serial one
+        kname = "sim_steps" if os.environ.get("PAXISIM_SERIAL") == "0" else "sim_serial"
         occ = sim.occupancy()
         desc.update({"tiles_per_cu": occ[0], "lds_per_tile": occ[1], "staged_msgs": occ[2]})
         desc.update({"clusters_per_gpu": args.clusters, "sim_steps_per_step": args.sim_steps,
@@ -422,7 +424,7 @@ def main():
             "kernel_ms_per_step": kms_max / args.steps,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": f"sim_steps<{abi.n_replicas(cfg)},{proto}>",
+                         "kernel": f"{kname}<{abi.n_replicas(cfg)},{proto}>",
                          "avg_launch_ms": avg_launch_ms, "launches": launches,
                          "alg_bytes_per_launch": alg_bytes(d) / max(1, launches)},
             "build_id": bid,
