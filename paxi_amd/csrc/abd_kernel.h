@@ -136,6 +136,7 @@ __device__ __forceinline__ void abd_handle_setreply(const Params& P, Rep<NT>& x,
 
 struct AbdProto {
   static constexpr uint32_t kind = PAXISIM_ABD;
+  static constexpr bool step_scratch = false;   // (no per-replica-step LDS scratch: sim_core.h sim_serial)
   template <int NT>
   __device__ static __forceinline__ void load(const Params& P, Rep<NT>& x) {
     const size_t i = rc(P, x.r, x.c);

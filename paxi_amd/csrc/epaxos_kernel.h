@@ -488,6 +488,7 @@ __device__ void ep_handle_commit(const Params& P, Rep<NT>& x, uint32_t o, const 
 
 struct EPaxosProto {
   static constexpr uint32_t kind = PAXISIM_EPAXOS;
+  static constexpr bool step_scratch = false;   // (no per-replica-step LDS scratch: sim_core.h sim_serial)
   template <int NT>
   __device__ static __forceinline__ void load(const Params& P, Rep<NT>& x) {
     const size_t i = rc(P, x.r, x.c);

@@ -923,6 +923,10 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
       P.J = 0;
       P.lds_tail = PXS_CLIENT_LDS ? P.img.off_wcur : P.img.off_poison;
       P.lds_bytes = base - P.lds_tail;
+      if (PXS_WP_SCRATCH && P.protocol == PAXISIM_WPAXOS && P.wlds) {   // the replica-step instance scratch (wpaxos_kernel.h)
+        P.off_wscr = base;
+        P.lds_bytes += P.keys * WP_WORDS * LANES * 4u;
+      }
     }
   }
   P.C = (cfg->clusters + LANES * P.G - 1) / (LANES * P.G) * (LANES * P.G);

@@ -125,6 +125,7 @@ struct Params {
   uint32_t J, off_stage;   // LDS stage: J staged picks per replica at LDS byte off_stage ([r][J][64] x 16 B)
   uint32_t lds_bytes;      // LDS per cluster group (16-B multiple): the image + the stage
   uint32_t lds_tail;       // serial kernel: the image bytes [lds_tail, bytes) are staged in LDS (PXS_CLIENT_LDS)
+  uint32_t off_wscr;       // serial kernel, WPaxos (wlds): LDS byte offset of the replica-step instance scratch [K][5][lane]
   uint32_t G;              // cluster groups (64-cluster tiles) per workgroup
   uint32_t rec_per_block;  // D*N*NS*M*64
   const DevFault* faults;
@@ -381,6 +382,13 @@ __device__ __forceinline__ void stamp_case(const Params& P, uint32_t blk, uint32
 // (0) or stages them into LDS with the mailbox counts (1, A/B).
 #ifndef PXS_CLIENT_LDS
 #define PXS_CLIENT_LDS 1   // (A/B r3: the HBM tables cost config 2 6%, configs 4 and 5 4%)
+#endif
+
+// The serial kernel's WPaxos replica-step scratch (wpaxos_kernel.h step_begin):
+// the current replica's instance scalars in LDS.  Off: the scratch costs more
+// in tiles per CU (8 -> 5 on config 5) than it saves (A/B r3: -35%).
+#ifndef PXS_WP_SCRATCH
+#define PXS_WP_SCRATCH 0
 #endif
 
 // ---- SoA addressing --------------------------------------------------------

@@ -390,6 +390,15 @@ __device__ __forceinline__ void kv_exec(const Params& P, Rep<NT>& x, uint32_t h,
 // kernel) each slot's iteration loads the next slot's flags before it issues
 // its own stores (PXS_EXEC_AHEAD), so the loop's exit test does not wait for
 // them (vmcnt retires loads and stores in issue order).
+// A WPaxos bind (wlds) does not load the instance's digest: exec, its only
+// reader, loads it on first use, and the unbind stores it only if exec changed it.
+template <int NT>
+__device__ __forceinline__ void digest_need(const Params& P, Rep<NT>& x) {
+  if (hbm_log(x) && P.wlds && x.dig_st == 0u) {
+    x.digest = P.wdig[(((size_t)x.blk * P.keys + x.key) * nrep<NT>(P) + x.r) * LANES + x.lane];
+    x.dig_st = 1u;
+  }
+}
 #ifndef PXS_EXEC_AHEAD
 #define PXS_EXEC_AHEAD 1
 #endif
@@ -410,12 +419,14 @@ __device__ __forceinline__ void paxos_exec(const Params& P, Rep<NT>& x, uint32_t
       nc = x.l_b[ni];
     }
     if (x.iflags & PAXISIM_F_WOVF) x.flags |= PAXISIM_F_UNFAITHFUL;
+    digest_need<NT>(P, x);
     const uint32_t cmd = c & CMD_MASK;
     const uint32_t h = P.kv ? wl_hash(x.kc, cmd) : 0u;
     const uint32_t key = P.kv ? kv_key<NT>(P, x, h, cmd) : 0u;
     if (c & (EF_REQSELF | EF_REQEXT))                             // Reply{Value: p.Execute(cmd)}, paxos.go:352-362
       request_reply<NT>(P, x, ereq<NT>(P, x, i, c), cmd, P.kv ? kv_get<NT>(P, x, key) : 0u);
     x.digest = mix64(x.digest ^ (((uint64_t)(uint32_t)x.execute << 32) | cmd));
+    x.dig_st = 2u;
     if (P.kv) kv_exec<NT>(P, x, h, key, cmd);                      // p.Execute(e.command), paxos.go:352
     set_b(x, i, 0u);                                               // delete(p.log, execute)
     x.execute++;
@@ -661,6 +672,7 @@ __device__ __forceinline__ bool p2b_absorb(const Params& P, Rep<NT>& x, uint32_t
 // ---------------------------------------------------------------------------
 struct PaxosProto {
   static constexpr uint32_t kind = PAXISIM_PAXOS;
+  static constexpr bool step_scratch = false;   // (no per-replica-step LDS scratch: sim_core.h sim_serial)
   template <int NT>
   __device__ static __forceinline__ void load(const Params& P, Rep<NT>& x) {
     const size_t i = rc(P, x.r, x.c);

@@ -52,6 +52,8 @@ struct Rep {
   uint8_t* l_cnt;
   uint8_t* l_agn;                       // agreement-ring arrivals this step, [parity][r][lane] (agree_post)
   uint32_t* l_inst;                     // WPaxos (wlds): instance scalars in LDS (wpaxos_kernel.h)
+  uint32_t ikst, iro;                   // WPaxos (wlds): word offsets of key k / this replica in l_inst
+  uint32_t dig_st;                      // WPaxos (wlds): bound instance's digest 0 not loaded, 1 loaded, 2 changed
   uint4* rec;                           // this block's record region
 };
 
@@ -1118,6 +1120,7 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
         x.flags = P.flags[i];
         x.kvver = P.kv ? P.kv_ver[i] : 0u;
         Proto::template load<NT>(P, x);
+        if constexpr (Proto::step_scratch) Proto::template step_begin<NT>(P, x, L + (P.off_wscr - tail));
         rep_counters_zero<NT>(x);
 #ifdef PXS_STAMPS
         Stamps st = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1139,6 +1142,7 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
         P.flags[i] = x.flags;
         if (P.kv) P.kv_ver[i] = x.kvver;
         Proto::template store<NT>(P, x);
+        if constexpr (Proto::step_scratch) Proto::template step_end<NT>(P, x);
         rep_counters_flush<NT>(P, x);
       }
     }

@@ -46,14 +46,13 @@ __device__ __forceinline__ void wp_bind(const Params& P, Rep<NT>& x, uint32_t ke
   const size_t si = wp_slot<NT>(P, x, key);
   uint4 a, b;
   if constexpr (LDS) {
-    const uint32_t* w = x.l_inst + (((key * nrep<NT>(P) + x.r) * WP_WORDS) << 6) + x.lane;
+    const uint32_t* w = x.l_inst + key * x.ikst + x.iro + x.lane;
     a = make_uint4(w[0], w[64], w[128], w[192]);
     b.w = w[256];
-    const uint64_t d = P.wdig[si];
     b.x = (a.w >> 4) & 0x3Fu;
     a.w &= 0xFFFF000Fu;
-    b.y = (uint32_t)d;
-    b.z = (uint32_t)(d >> 32);
+    b.y = b.z = 0u;                  // the digest: loaded by exec when it needs it (digest_need)
+    x.dig_st = 0u;
   } else {
     a = P.wst[2 * si];
     b = P.wst[2 * si + 1];
@@ -70,6 +69,7 @@ __device__ __forceinline__ void wp_bind(const Params& P, Rep<NT>& x, uint32_t ke
   x.p1mask = a.w >> 16;
   x.npend = b.x;
   x.digest = (uint64_t)b.y | ((uint64_t)b.z << 32);
+  if constexpr (!LDS) x.dig_st = 1u;
   x.pol = b.w & 0xFFFFu;
   x.cmask = b.w >> 16;
   uint32_t* lb = P.wlog + si * P.W * 4u;
@@ -85,13 +85,13 @@ __device__ __forceinline__ void wp_unbind(const Params& P, const Rep<NT>& x) {
   const size_t si = wp_slot<NT>(P, x, x.key);
   const uint32_t meta = (x.active & 1u) | (x.exists << 1) | (x.iflags << 2) | (x.p1mask << 16);
   if constexpr (LDS) {
-    uint32_t* w = x.l_inst + (((x.key * nrep<NT>(P) + x.r) * WP_WORDS) << 6) + x.lane;
+    uint32_t* w = x.l_inst + x.key * x.ikst + x.iro + x.lane;
     w[0] = x.ballot;
     w[64] = (uint32_t)x.slot;
     w[128] = (uint32_t)x.execute;
     w[192] = meta | (x.npend << 4);
     w[256] = x.pol | (x.cmask << 16);
-    P.wdig[si] = x.digest;
+    if (x.dig_st == 2u) P.wdig[si] = x.digest;
   } else {
     P.wst[2 * si] = make_uint4(x.ballot, (uint32_t)x.slot, (uint32_t)x.execute, meta);
     P.wst[2 * si + 1] = make_uint4(x.npend, (uint32_t)x.digest, (uint32_t)(x.digest >> 32), x.pol | (x.cmask << 16));
@@ -245,6 +245,8 @@ struct WPaxosProtoT {
   template <int NT>
   __device__ static __forceinline__ void load(const Params& P, Rep<NT>& x) {
     x.l_inst = x.l_a;                // image region a: the instance scalars (LDS layout)
+    x.ikst = (nrep<NT>(P) * WP_WORDS) << 6;
+    x.iro = (x.r * WP_WORDS) << 6;
     x.nfwd = P.nfwd[rc(P, x.r, x.c)];
     x.e0 = 0;                        // entry of slot s: word 4*(s & (W-1)) of the lane's window
     x.es = 4;
@@ -255,6 +257,35 @@ struct WPaxosProtoT {
   template <int NT>
   __device__ static __forceinline__ void store(const Params& P, const Rep<NT>& x) {
     P.nfwd[rc(P, x.r, x.c)] = x.nfwd;
+  }
+  // The serial kernel (sim_core.h) runs one replica at a time: the instance
+  // scalars of that replica's K kpaxos move from the HBM image into an LDS
+  // scratch [key][word][lane] for its replica-step (one coalesced copy each
+  // way), so a bind / unbind is LDS traffic rather than eight keys' worth of
+  // scattered HBM rows per wave.
+  static constexpr bool step_scratch = LDS && PXS_WP_SCRATCH;
+  template <int NT>
+  __device__ static __forceinline__ void step_begin(const Params& P, Rep<NT>& x, uint8_t* scr) {
+    uint32_t* s = reinterpret_cast<uint32_t*>(scr);
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(P.image + (size_t)x.blk * P.img.bytes + P.img.off_a) +
+                        ((x.r * WP_WORDS) << 6) + x.lane;
+    const uint32_t gk = (nrep<NT>(P) * WP_WORDS) << 6;
+    for (uint32_t k = 0; k < P.keys; k++)
+#pragma unroll
+      for (uint32_t w = 0; w < WP_WORDS; w++) s[((k * WP_WORDS + w) << 6) + x.lane] = g[k * gk + (w << 6)];
+    x.l_inst = s;
+    x.ikst = WP_WORDS << 6;
+    x.iro = 0;
+  }
+  template <int NT>
+  __device__ static __forceinline__ void step_end(const Params& P, const Rep<NT>& x) {
+    const uint32_t* s = x.l_inst;
+    uint32_t* g = reinterpret_cast<uint32_t*>(P.image + (size_t)x.blk * P.img.bytes + P.img.off_a) +
+                  ((x.r * WP_WORDS) << 6) + x.lane;
+    const uint32_t gk = (nrep<NT>(P) * WP_WORDS) << 6;
+    for (uint32_t k = 0; k < P.keys; k++)
+#pragma unroll
+      for (uint32_t w = 0; w < WP_WORDS; w++) g[k * gk + (w << 6)] = s[((k * WP_WORDS + w) << 6) + x.lane];
   }
   template <int NT>
   __device__ static __forceinline__ void client_request(const Params& P, Rep<NT>& x, uint32_t cid) {
