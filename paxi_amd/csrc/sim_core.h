@@ -42,6 +42,7 @@ struct Rep {
   uint32_t client, sent, dropped, discarded, commits, replies;
   uint32_t kvver;                       // database.version (P.kv)
   uint32_t send_seq;
+  uint32_t rw, rv;                      // a client reply's value not yet stored: worker + 1 (0 = none), value
   uint32_t dmask, fmask;                // per-step: dropped / flaky destinations
   uint32_t im;                          // pending send intent: destination mask (0 = none)
   uint32_t iw0, iw1, iw2, iw3;          // pending send intent: the record
@@ -346,6 +347,19 @@ __device__ __forceinline__ bool wl_write(const Params& P, uint32_t kc, uint32_t 
 #ifndef PXS_REPLY_STORE
 #define PXS_REPLY_STORE 1   // 0: the worker's last Reply.Value is not kept (A/B attribution only)
 #endif
+#ifndef PXS_REPLY_DEFER
+#define PXS_REPLY_DEFER 1   // the Reply.Value store waits until the end of the merge trip
+#endif
+// The value usually comes from a load issued just before the reply (Execute's
+// previous value, paxos_kernel.h kv_get): storing it at the end of the trip
+// lets the handler go on without waiting for that load.
+template <int NT>
+__device__ __forceinline__ void reply_flush(const Params& P, Rep<NT>& x) {
+  if (x.rw) {
+    P.wrep[(size_t)(x.rw - 1u) * P.C + x.c] = x.rv;
+    x.rw = 0;
+  }
+}
 // The HTTP response reaches worker w, which keeps its Reply.Value (the value
 // a read returned, benchmark.go:259-262) and issues its next request: it
 // arrives at the worker's target (client source N) in the next step.
@@ -356,7 +370,13 @@ __device__ __forceinline__ void client_reply(const Params& P, Rep<NT>& x, uint32
   const uint32_t wi = (w << 6) | x.lane;
   if (x.l_wcur[wi] != cid) return;              // duplicate reply: the worker moved on
   x.replies++;
-  if (PXS_REPLY_STORE) P.wrep[(size_t)w * P.C + x.c] = value;
+  if (PXS_REPLY_STORE && PXS_REPLY_DEFER) {
+    reply_flush<NT>(P, x);
+    x.rw = w + 1u;
+    x.rv = value;
+  } else if (PXS_REPLY_STORE) {
+    P.wrep[(size_t)w * P.C + x.c] = value;
+  }
   const uint32_t issued = x.l_wiss[wi];
   if (P.max_requests == 0 || issued < P.max_requests) {
     const uint64_t nc = 1ull + w + (uint64_t)P.WK * issued;
@@ -510,6 +530,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
   x.send_seq = 0;
   x.stop = false;
   x.im = 0;
+  x.rw = 0;
   x.hs = step_key(x.kc, x.t);
   if (P.late_workers) client_start<NT>(P, x);
   {
@@ -752,6 +773,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
     // stores, and waiting for them does not wait for the stores (vmcnt
     // retires loads and stores in issue order).
     PXS_SUB_T0(pxs_fl0)
+    reply_flush<NT>(P, x);
     intent_flush<NT>(P, x);
     if constexpr (Proto::kind == PAXISIM_PAXOS) { PXS_SUB_T1(pxs_fl0, 13) }
 #endif
@@ -773,6 +795,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
     }
     i++;
   }
+  reply_flush<NT>(P, x);
 #pragma unroll
   for (uint32_t s = 0; s < NSMAX; s++)
     if (s < NS) x.l_cnt[((box0 + s) << 6) | x.lane] = 0;
