@@ -280,13 +280,22 @@ struct LinCheck {
       if (m != LIN_NOV) merge(r, m);
       bool cyc = false;
       uint64_t gray = 0;
+      const bool was_cyclic = maybe_cyclic;
       if (maybe_cyclic) cyc = cycle(gray);
       else if (m != LIN_NOV && reaches_self(m)) cyc = cycle(gray);
       if (cyc) {
         anomalies++;
         cut(gray);
-        uint64_t g2;
-        maybe_cyclic = cycle(g2);                        // still cyclic: Cycle() at every read
+        // still cyclic: Cycle() at every read.  When the graph was acyclic
+        // before this read's merge, every cycle runs through the merged vertex
+        // m (the merge's edges s -> m are the only new ones), so a reach from
+        // m decides it; otherwise the full DFS does.
+        if (!was_cyclic) {
+          maybe_cyclic = reaches_self(m);
+        } else {
+          uint64_t g2;
+          maybe_cyclic = cycle(g2);
+        }
       } else {
         maybe_cyclic = false;
       }
@@ -297,13 +306,18 @@ struct LinCheck {
 
 // Stable sort of src[0, n) by start into s.ops (sort.Sort(byTime): ties keep
 // canonical order): each op's rank counts the ops before it.
+// The start times are first copied into the scratch's stack array (free
+// until run()), so the n^2 rank comparisons read the scratch, not the stage.
 template <bool G>
 __device__ inline void lin_sort(const uint4* src, uint32_t n, LinScratch& s) {
+  for (uint32_t i = lane_id(); i < n; i += 64u) s.stk[i] = src[i].z;
+  if (G) __threadfence_block();
+  __builtin_amdgcn_wave_barrier();
   for (uint32_t i = lane_id(); i < n; i += 64u) {
     const uint4 o = src[i];
     uint32_t rk = 0;
     for (uint32_t j = 0; j < n; j++) {
-      const uint32_t sj = src[j].z;
+      const uint32_t sj = s.stk[j];
       rk += (sj < o.z || (sj == o.z && j < i)) ? 1u : 0u;
     }
     s.ops[rk] = o;
