@@ -47,7 +47,7 @@ DEFAULTS = {1: dict(clusters=1, sim_steps=3010, window=32, mbox=16),
             3: dict(clusters=1 << 20, sim_steps=80, window=16, mbox=16),
             4: dict(clusters=1 << 19, sim_steps=200, window=16, mbox=24),
             5: dict(clusters=1 << 18, sim_steps=200, window=16, mbox=24)}
-LAUNCH_STEPS = 50   # virtual steps fused per kernel launch
+LAUNCH_STEPS = int(os.environ.get("PAXISIM_LAUNCH_STEPS", "50"))   # virtual steps fused per kernel launch
 
 
 def alg_bytes(delta):
