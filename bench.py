@@ -18,7 +18,6 @@ Multi-GPU: see paxi_amd/dist.py — clusters shard by range, no data-path
 collective; RCCL all-reduces the statistics and the max time.
 """
 import argparse
-import hashlib
 import json
 import os
 import sys
@@ -62,13 +61,16 @@ def stats_delta(a, b):
 
 
 def build_id():
-    """Fingerprint of the HIP product sources and flags (what a traffic record was measured on)."""
+    """The source fingerprint compiled into the loaded libpaxisim.so
+    (paxisim_build_id): the binary this run measured, not the tree beside it."""
+    from paxi_amd import sim as psim
+    return psim.build_id()
+
+
+def source_id():
+    """Fingerprint of the HIP sources in this tree (what build() would compile)."""
     import __graft_entry__ as ge
-    h = hashlib.sha256(" ".join(ge.HIP_FLAGS).encode())
-    for f in sorted(set(ge.HIP_SOURCES + ge.HIP_HEADERS)):
-        with open(os.path.join(ROOT, ge.CSRC, f), "rb") as fh:
-            h.update(f.encode() + fh.read())
-    return h.hexdigest()[:16]
+    return ge.source_id()
 
 
 def workload(cfg_id, clusters, base, device, args):
@@ -108,17 +110,24 @@ def workload(cfg_id, clusters, base, device, args):
         # (replica 3), whose first request runs phase 1 under -ephemeral_leader
         # (paxos/replica.go:61) and re-elects it.  The first set stays blocked on
         # the crashed leader: Paxi's HTTP client has no retry.
+        # --fz 1: FGridQ1/Q2(1) (quorum.go:99-119); --fz 0: the Grid variant,
+        # GridRow/GridColumn (quorum.go:85-97), Q1 = Q2 = 3 replicas at 3x3
         c = args.crash_step
-        cfg = abi.make_config(npz=[3, 3, 3], clusters=clusters, cluster_base=base, seed=42, q1=abi.Q_FGRID_Q1,
-                              q2=abi.Q_FGRID_Q2, fz=1, ephemeral_leader=1, window=args.window, mbox_cap=args.mbox,
+        fz = getattr(args, "fz", 1)
+        q1, q2 = (abi.Q_FGRID_Q1, abi.Q_FGRID_Q2) if fz else (abi.Q_GRID_ROW, abi.Q_GRID_COLUMN)
+        cfg = abi.make_config(npz=[3, 3, 3], clusters=clusters, cluster_base=base, seed=42, q1=q1,
+                              q2=q2, fz=fz, ephemeral_leader=1, window=args.window, mbox_cap=args.mbox,
                               max_delay=0, steps_per_launch=LAUNCH_STEPS, device=device,
                               kv=args.kv)
         wl = abi.make_workload(outstanding=8, target=[0, 0, 0, 0, 3, 3, 3, 3], start_step=[0, 0, 0, 0, c, c, c, c])
         faults = [abi.make_fault(abi.FAULT_CRASH, 0, step_from=c)]
         return cfg, wl, None, faults, {
-            "workload": "BASELINE config 4: FGrid 3x3 (fz=1) x 512K clusters/GPU; leader 1.1 crashes for good at "
+            "workload": (f"BASELINE config 4: FGrid 3x3 (fz={fz})" if fz else
+                         "BASELINE config 4, Grid variant: 3x3 GridRow/GridColumn (fz=0)") +
+                        f" x 512K clusters/GPU; leader 1.1 crashes for good at "
                         f"step {c}, clients then turn to 2.1 which re-elects itself (ephemeral leader)",
-            "replicas": 9, "outstanding": "4 -> 1.1 from step 0, 4 -> 2.1 from the crash", "crash_step": c}
+            "replicas": 9, "outstanding": "4 -> 1.1 from step 0, 4 -> 2.1 from the crash", "crash_step": c,
+            "fz": fz}
     if cfg_id == 5:
         cfg = abi.make_config(protocol=abi.WPAXOS, npz=[3, 3, 3], keys=8, fz=0, adaptive=1, policy_threshold=3,
                               clusters=clusters, cluster_base=base, seed=42, window=args.window, mbox_cap=args.mbox,
@@ -149,7 +158,8 @@ def measured_traffic(args, kernel, mbox, bid):
     same = (t.get("kernel") == kernel and t.get("clusters_per_gpu") == args.clusters
             and t.get("sim_steps_per_step") == args.sim_steps and t.get("window") == args.window
             and t.get("mbox_cap") == mbox and t.get("build_id") == bid
-            and t.get("warmup") == args.warmup and t.get("steps") == args.steps)
+            and t.get("warmup") == args.warmup and t.get("steps") == args.steps
+            and (args.config != 4 or t.get("fz", 1) == getattr(args, "fz", 1)))
     if not same:
         return None
     return {"bytes_per_launch": t["bytes_per_launch"], "source": os.path.relpath(path, ROOT),
@@ -282,6 +292,8 @@ def main():
     ap.add_argument("--window", type=int, default=None)
     ap.add_argument("--mbox", type=int, default=None)
     ap.add_argument("--history", type=int, default=512, help="config 3: ops recorded per replica")
+    ap.add_argument("--fz", type=int, default=1, choices=[0, 1],
+                    help="config 4: FGrid fz (1) or the Grid variant GridRow/GridColumn (0)")
     ap.add_argument("--crash-step", type=int, default=None,
                     help="config 4: step of the leader crash (default: the first timed step)")
     ap.add_argument("--kv", type=int, default=1, choices=[0, 1],
@@ -335,6 +347,7 @@ def main():
         sim.step(args.sim_steps)
     sim.sync()
     s0 = sim.stats().as_dict()
+    active_start = sim.active_clusters()
     sim.kernel_time(reset=True)
 
     barrier()
@@ -377,7 +390,8 @@ def main():
 
     st1 = sim.stats()
     vals = pdist.stats_counters(d, alg_bytes(d), violations, s1["flagged"], agree_compared=st1.agree_compared,
-                                agree_missed=st1.agree_missed, active=sim.active_clusters())
+                                agree_missed=st1.agree_missed, active=sim.active_clusters(),
+                                active_start=active_start)
     if pd is not None:
         tot, (dt_max, kms_max) = pdist.reduce_counters_abi(pd, vals, [dt, kms])
     else:
@@ -416,7 +430,12 @@ def main():
             "agreement_coverage": {"checkpoints_compared": int(tot["agree_compared"]),
                                    "checkpoints_missed": int(tot["agree_missed"]),
                                    "every": "16 executed slots, against the first executor (paxisim_check)"},
+            "active_clusters_start": int(tot["active_start"]),
             "active_clusters_end": int(tot["active"]),
+            # the live set shrinks over the window (no-retry semantics): the rate per
+            # live cluster (mean of the window's start and end counts) compares runs across that decay
+            "msgs_per_s_per_live_cluster": tot["delivered_total"] / dt_max /
+                                           max(1.0, 0.5 * (tot["active_start"] + tot["active"])),
             "unfaithful_clusters": int(tot["flag_UNFAITHFUL"]),
             "poisoned_clusters": int(tot["flag_POISON"]),
             "flagged_clusters": {n: int(tot["flag_" + n]) for n in FLAG_NAMES},
@@ -428,6 +447,8 @@ def main():
                          "avg_launch_ms": avg_launch_ms, "launches": launches,
                          "alg_bytes_per_launch": alg_bytes(d) / max(1, launches)},
             "build_id": bid,
+            "build_id_of": "the loaded libpaxisim.so (paxisim_build_id)",
+            "build_matches_sources": bid == source_id(),
         }
         tr = measured_traffic(args, out["roofline"]["kernel"], cfg.mbox_cap, bid)
         if tr is not None:

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PAXISIM_ABI_VERSION 12
+#define PAXISIM_ABI_VERSION 13
 
 #define PAXISIM_MAX_N        16  /* replicas per cluster (ack masks are u16) */
 #define PAXISIM_MAX_ZONES    16
@@ -169,8 +169,15 @@ typedef struct paxisim_config {
 } paxisim_config;
 
 /* Key distributions of the benchmark's key generator (benchmark.go:202-244,
- * Bconfig.Distribution).  Keys live in [0, keys); the key of a command is a
- * pure function of (cluster, cid), so both backends agree. */
+ * Bconfig.Distribution).  Key indices live in [0, keys); the key of a command
+ * is a pure function of (cluster, cid), so both backends agree (DESIGN.md
+ * §3.8).  The key *value* the reference's Database sees is key_min + index for
+ * "order", "uniform" and "conflict" (Go adds Bconfig.Min), the index itself for
+ * the table distributions (Go adds no Min there), and 0 for "conflict"'s
+ * literal key 0 (benchmark.go:213-214), which has its own index key_space when
+ * key_min != 0.  A table draw beyond [0, keys) ("exponential" is unbounded in
+ * Go) is not folded: the replica that needs the key raises PAXISIM_F_UNFAITHFUL
+ * and uses index keys-1. */
 enum paxisim_distribution {
   PAXISIM_DIST_UNIFORM  = 0,  /* "uniform": rand.Intn(K) (benchmark.go:210-211)         */
   PAXISIM_DIST_ORDER    = 1,  /* "order": counter+1 mod K, counter = cid (205-207)      */
@@ -192,8 +199,23 @@ typedef struct paxisim_workload {
   uint32_t start_step[PAXISIM_MAX_WORKERS]; /* step at which worker w's first request reaches
                                  target[w] (0 = at creation): e.g. clients that turn to
                                  another replica after a crash (BASELINE config 4) */
-  uint32_t key_min;           /* Bconfig.Min (benchmark.go:34): the key value of key index 0; only
-                                 KPaxos' static leader assignment reads key values */
+  uint32_t key_min;           /* Bconfig.Min (benchmark.go:34): the key value of index 0 for ORDER,
+                                 UNIFORM and CONFLICT; only KPaxos' static leader assignment (and
+                                 trace export) reads key values */
+  uint32_t key_space;         /* Bconfig.K of ORDER / UNIFORM / CONFLICT: their counter and draw
+                                 range over indices [0, key_space) (0 = keys); CONFLICT with
+                                 key_min != 0 puts the literal key 0 at index key_space (needs
+                                 key_space < keys) */
+  uint32_t key_tail;          /* TABLE: a u32 draw >= key_tail (when nonzero) is a key beyond the
+                                 key space (the "exponential" tail): not folded, see above */
+  uint32_t move_every;        /* TABLE with Bconfig.Move (benchmark.go:137-140): Mu moves once per
+                                 move_every issued commands, i.e. command cid draws from table
+                                 e = (cid-1) / move_every of the Mu sequence (0 = Mu fixed) */
+  uint32_t move_tables;       /* tables in move_cdf: table e holds the key CDF for the e-th Mu */
+  uint32_t move_loop;         /* after the last table the Mu sequence repeats from this one:
+                                 e >= move_tables uses move_loop + (e - move_loop) % (move_tables - move_loop) */
+  const uint32_t* move_cdf;   /* move_tables x PAXISIM_MAX_KEYS thresholds (copied at create); each
+                                 table as key_cdf: non-decreasing over [0, keys-1) */
 } paxisim_workload;
 
 /* Random fault process, applied per (cluster, src, dst) link every step. */
@@ -316,6 +338,9 @@ typedef struct paxisim paxisim;   /* opaque handle */
 
 int  paxisim_abi_version(void);
 const char* paxisim_last_error(void);
+/* Fingerprint of the HIP sources and compile flags this library was built
+ * from (__graft_entry__.source_id), so a measurement names its binary. */
+const char* paxisim_build_id(void);
 
 /* Create a handle.  All clusters start at step 0 with empty state; worker w's
  * first request is waiting at its target replica at step 0. */
@@ -400,8 +425,9 @@ int  paxisim_kernel_time(paxisim* h, double* ms, uint64_t* launches, int reset);
 
 /* History.Linearizable (history.go:55-71, checker.go:69-104) over every
  * (cluster, key) of the recorded ABD operations: anomalous reads, operations
- * checked, and partitions skipped because they exceed the checker's 128-op
- * graph (any pointer may be NULL). */
+ * checked, and partitions skipped because they exceed the checker's bit sets
+ * (more than 16384 ops in one (cluster, key); their ops are not in `ops`).
+ * Any pointer may be NULL. */
 int  paxisim_linearizable(paxisim* h, uint64_t* anomalies, uint64_t* ops, uint64_t* skipped);
 
 /* Completed ABD operations of one local cluster: 5 words per op {key,

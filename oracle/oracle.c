@@ -258,6 +258,7 @@ struct oracle_sim {
   uint32_t zfirst[PAXISIM_MAX_ZONES]; /* replica index of "z.1" */
   uint32_t AR;                     /* agreement ring: checkpoints kept per (cluster, instance) */
   int kv;                          /* replicas keep the Database (paxisim_config.kv) */
+  uint32_t* move_cdf;              /* moving-Mu key CDF tables (a copy of paxisim_workload.move_cdf) */
 };
 
 /* handler context: one replica of one cluster at one step */
@@ -564,6 +565,7 @@ static void replica_handle_request(ctx_t* x, uint32_t req) {
 static void paxos_exec(ctx_t* x);
 static void agree_arrive(ctx_t* x, uint32_t k);
 static inline uint32_t wl_key(const struct oracle_sim* s, uint32_t kc, uint32_t cid);
+static inline uint32_t key_fit(ctx_t* x, uint32_t k);
 static inline int wl_write(const struct oracle_sim* s, uint32_t kc, uint32_t cid);
 
 static void paxos_handle_p1a(ctx_t* x, uint32_t mb) {      /* paxos.go:134-162 */
@@ -778,18 +780,27 @@ static void agree_arrive(ctx_t* x, uint32_t k) {
   if (*a != want) x->n->agb++;
 }
 
+/* The key of an executed command when replicas keep the Database: a per-key
+ * instance (WPaxos, M2Paxos, KPaxos) executes only commands of its own key;
+ * otherwise the workload's key, fitted to the key space. */
+static uint32_t exec_key(ctx_t* x, uint32_t cmd) {
+  if (!x->s->kv) return 0u;
+  if (x->s->cfg.protocol == PAXISIM_WPAXOS) return x->ktag >> 16;
+  return key_fit(x, wl_key(x->s, x->c->kc, cmd));
+}
+
 /* Database.Execute's return value (db.go:103-114): the key's value before the
  * command (0 = nil), the Reply.Value of an executed request. */
-static uint32_t kv_get(ctx_t* x, uint32_t cmd) {
-  return x->s->kv ? x->n->db[wl_key(x->s, x->c->kc, cmd)] : 0u;
+static uint32_t kv_get(ctx_t* x, uint32_t key) {
+  return x->s->kv ? x->n->db[key] : 0u;
 }
 
 /* Database.Execute (db.go:103-114) when replicas keep the KV: a write's value
  * (its command id) goes to its key, database.version counts it (put,
  * db.go:123-134); a read changes nothing. */
-static void kv_exec(ctx_t* x, uint32_t cmd) {
+static void kv_exec(ctx_t* x, uint32_t key, uint32_t cmd) {
   if (!x->s->kv || !wl_write(x->s, x->c->kc, cmd)) return;
-  x->n->db[wl_key(x->s, x->c->kc, cmd)] = cmd;
+  x->n->db[key] = cmd;
   x->n->db_version++;
 }
 
@@ -799,12 +810,13 @@ static void paxos_exec(ctx_t* x) {                         /* paxos.go:345-369 *
     entry_t* e = log_at(x, p->execute);
     if (!(e->meta & E_EXISTS) || !(e->meta & E_COMMIT)) break;
     if (x->p->iflags & PAXISIM_F_WOVF) raise_flag(x, PAXISIM_F_UNFAITHFUL);
+    const uint32_t key = exec_key(x, e->cmd);
     if (e->req) {                                          /* Reply{Value: p.Execute(...)}: the previous value */
-      request_reply(x, e->req, e->cmd, kv_get(x, e->cmd));
+      request_reply(x, e->req, e->cmd, kv_get(x, key));
       e->req = 0;
     }
     p->digest = mix64(p->digest ^ (((uint64_t)(uint32_t)p->execute << 32) | e->cmd));
-    kv_exec(x, e->cmd);                                    /* p.Execute(e.command), paxos.go:352 */
+    kv_exec(x, key, e->cmd);                               /* p.Execute(e.command), paxos.go:352 */
     if (x->s->keep_xlog) {
       if (p->nx == p->capx) {
         p->capx = p->capx ? 2 * p->capx : 1024;
@@ -849,6 +861,7 @@ static inline uint32_t wl_hash(uint32_t kc, uint32_t cid) { return fmix32(fmix32
  * z of the replica it sends to, otherwise uniform over all keys. */
 static inline uint32_t wl_key(const struct oracle_sim* s, uint32_t kc, uint32_t cid) {
   const uint32_t h = wl_hash(kc, cid), K = s->cfg.keys;
+  const uint32_t KS = s->wl.key_space ? s->wl.key_space : K;   /* Bconfig.K of order/uniform/conflict */
   if (s->wl.locality_ppm) {
     const uint32_t w = (cid - 1u) % s->wl.outstanding;
     const uint32_t z = s->zone_of[s->wl.target[w]] - 1u, Z = s->Z;
@@ -856,20 +869,54 @@ static inline uint32_t wl_key(const struct oracle_sim* s, uint32_t kc, uint32_t 
     if (nk && ppm_hit(fmix32(h ^ 0x165667B1u), s->wl.locality_ppm)) return z + Z * (h % nk);
   }
   /* Bconfig.Distribution (benchmark.go:202-233) as a function of cid:
-   * "order" counter+1 mod K with the counter = cid (205-207); "conflict" key 0
-   * with rand.Intn(100) < Conflicts, else order (213-219); "normal", "zipfan",
-   * "exponential" (221-233) by inverse CDF over the caller's key_cdf table. */
+   * "order" counter+1 mod K with the counter = cid (205-207); "conflict" the
+   * literal key 0 with rand.Intn(100) < Conflicts (213-214: no Min added, so
+   * with Min != 0 it is a key of its own, index KS), else order (216-217);
+   * "normal", "zipfan", "exponential" (221-233) by inverse CDF over the
+   * caller's table.  A draw at or above key_tail lies beyond the key space
+   * (Go's "exponential" is unbounded): index K, flagged by key_fit.  With
+   * Bconfig.Move (137-140) Mu steps once per move_every issued commands: cid
+   * draws from table (cid-1)/move_every of the Mu sequence. */
   switch (s->wl.distribution) {
-    case PAXISIM_DIST_ORDER: return cid % K;
-    case PAXISIM_DIST_CONFLICT: return fmix32(h ^ 0x3C6EF372u) % 100u < s->wl.conflicts ? 0u : cid % K;
+    case PAXISIM_DIST_ORDER: return cid % KS;
+    case PAXISIM_DIST_CONFLICT:
+      return fmix32(h ^ 0x3C6EF372u) % 100u < s->wl.conflicts ? (s->wl.key_min ? KS : 0u) : cid % KS;
     case PAXISIM_DIST_TABLE: {
       const uint32_t u = fmix32(h ^ 0x2545F491u);
+      const uint32_t* cdf = s->wl.key_cdf;
       uint32_t k = 0, i;
-      for (i = 0; i + 1u < K; i++) k += u >= s->wl.key_cdf[i] ? 1u : 0u;
+      if (s->wl.move_every) {
+        uint32_t e = (cid - 1u) / s->wl.move_every;
+        if (e >= s->wl.move_tables) e = s->wl.move_loop + (e - s->wl.move_loop) % (s->wl.move_tables - s->wl.move_loop);
+        cdf = s->move_cdf + (size_t)e * PAXISIM_MAX_KEYS;
+      } else if (s->wl.key_tail && u >= s->wl.key_tail) {
+        return K;
+      }
+      for (i = 0; i + 1u < K; i++) k += u >= cdf[i] ? 1u : 0u;
       return k;
     }
-    default: return h % K;
+    default: return h % KS;
   }
+}
+/* The key value the reference's Database sees for index k (paxisim.h): Min +
+ * k for order/uniform/conflict, k itself for the table distributions (Go adds
+ * no Min), 0 for conflict's literal key. */
+static inline uint32_t key_value(const struct oracle_sim* s, uint32_t k) {
+  if (s->wl.distribution == PAXISIM_DIST_TABLE) return k;
+  if (s->wl.distribution == PAXISIM_DIST_CONFLICT && s->wl.key_min &&
+      k == (s->wl.key_space ? s->wl.key_space : s->cfg.keys))
+    return 0u;
+  return s->wl.key_min + k;
+}
+/* A key the replica uses: a draw beyond the key space has no state here (in Go
+ * it would be a new map entry), so the replica raises UNFAITHFUL and uses the
+ * last index. */
+static inline uint32_t key_fit(ctx_t* x, uint32_t k) {
+  if (k >= x->s->cfg.keys) {
+    raise_flag(x, PAXISIM_F_UNFAITHFUL);
+    k = x->s->cfg.keys - 1u;
+  }
+  return k;
 }
 static inline int wl_write(const struct oracle_sim* s, uint32_t kc, uint32_t cid) {
   return ppm_hit(fmix32(wl_hash(kc, cid) ^ 0x27D4EB2Fu), s->wl.write_ppm);
@@ -976,10 +1023,10 @@ static uint32_t kp_leader(const struct oracle_sim* s, uint32_t key) {
 
 static void wp_handle_request(ctx_t* x, uint32_t req) {   /* replica.go:42-66 */
   const struct oracle_sim* s = x->s;
-  const uint32_t key = wl_key(s, x->c->kc, REQ_CID(req));
+  const uint32_t key = key_fit(x, wl_key(s, x->c->kc, REQ_CID(req)));
   wp_init(x, key);
   if (s->variant == PAXISIM_KPAXOS) {                      /* kpaxos/replica.go:52-62 */
-    const uint32_t leader = kp_leader(s, s->wl.key_min + key);
+    const uint32_t leader = kp_leader(s, key_value(s, key));
     if (leader == x->r) paxos_handle_request(x, req);
     else node_forward(x, leader, req);                     /* `go r.Forward(leader, m)` */
     return;
@@ -1060,7 +1107,7 @@ static int ep_where(ctx_t* x, uint32_t o, int32_t s, ep_inst_t** out) {
 static inline int32_t* ep_cf(ctx_t* x, uint32_t o, uint32_t key) {       /* {slot (-1 none), seq} */
   return &x->n->ep_cf[((size_t)o * x->s->cfg.keys + key) * 2u];
 }
-static inline uint32_t ep_key(ctx_t* x, uint32_t cmd) { return wl_key(x->s, x->c->kc, cmd); }
+static inline uint32_t ep_key(ctx_t* x, uint32_t cmd) { return key_fit(x, wl_key(x->s, x->c->kc, cmd)); }
 
 /* the current seq of instance (o, d), the slot conflicts[o][key] names */
 static int32_t ep_seq_of(ctx_t* x, uint32_t o, int32_t d, uint32_t key) {
@@ -1135,8 +1182,9 @@ static void ep_execute(ctx_t* x) {
       p->inst[0].digest = mix64(p->inst[0].digest ^ (((uint64_t)((id << 24) | (uint32_t)sl) << 32) | i->cmd));
       p->ep_execs++;
       {
-        const uint32_t v = kv_get(x, i->cmd);               /* v := r.Execute(i.cmd), replica.go:373 */
-        kv_exec(x, i->cmd);
+        const uint32_t key = exec_key(x, i->cmd);
+        const uint32_t v = kv_get(x, key);                  /* v := r.Execute(i.cmd), replica.go:373 */
+        kv_exec(x, key, i->cmd);
         if (i->req) ep_reply(x, i, v);
       }
       if (s->keep_xlog) {
@@ -1369,7 +1417,7 @@ static inline void abd_put(replica_t* p, uint32_t key, uint32_t val) { if (val) 
 
 static void abd_handle_request(ctx_t* x, uint32_t cid) {                    /* abd/replica.go:50-71 */
   replica_t* p = x->n;
-  const uint32_t k = wl_key(x->s, x->c->kc, cid);
+  const uint32_t k = key_fit(x, wl_key(x->s, x->c->kc, cid));
   abd_op_t* e;
   p->abd_cid++;
   e = &p->ops[p->abd_cid & (x->s->OW - 1u)];
@@ -1600,9 +1648,30 @@ static int check_config(const paxisim_config* cfg, const paxisim_workload* wl,
   if (wl->outstanding > cfg->mbox_cap) return fail(PAXISIM_EINVAL, "outstanding exceeds mbox_cap");
   if (wl->distribution > PAXISIM_DIST_TABLE) return fail(PAXISIM_EINVAL, "distribution %u", wl->distribution);
   if (wl->distribution == PAXISIM_DIST_CONFLICT && wl->conflicts > 100) return fail(PAXISIM_EINVAL, "conflicts > 100");
-  if (wl->distribution == PAXISIM_DIST_TABLE)
-    for (w = 1; w + 1u < cfg->keys; w++)
-      if (wl->key_cdf[w] < wl->key_cdf[w - 1]) return fail(PAXISIM_EINVAL, "key_cdf must be non-decreasing");
+  {   /* the workload's key space (paxisim.h paxisim_workload) */
+    const uint32_t K = cfg->keys ? cfg->keys : 1u, KS = wl->key_space ? wl->key_space : K;
+    uint32_t e;
+    if (KS > K) return fail(PAXISIM_EINVAL, "key_space %u exceeds keys %u", KS, K);
+    if (wl->distribution == PAXISIM_DIST_CONFLICT && wl->key_min && KS >= K)
+      return fail(PAXISIM_EINVAL, "conflict with key_min != 0 needs key_space < keys (literal key 0 has its own index)");
+    if (wl->distribution == PAXISIM_DIST_TABLE) {
+      for (w = 1; w + 1u < K; w++)
+        if (wl->key_cdf[w] < wl->key_cdf[w - 1]) return fail(PAXISIM_EINVAL, "key_cdf must be non-decreasing");
+      if (wl->key_tail && K >= 2 && wl->key_tail < wl->key_cdf[K - 2])
+        return fail(PAXISIM_EINVAL, "key_tail below the last key_cdf threshold");
+    } else if (wl->key_tail) {
+      return fail(PAXISIM_EINVAL, "key_tail needs a table distribution");
+    }
+    if (wl->move_every) {
+      if (wl->distribution != PAXISIM_DIST_TABLE) return fail(PAXISIM_EINVAL, "move_every needs a table distribution");
+      if (!wl->move_cdf || wl->move_tables < 1 || wl->move_loop >= wl->move_tables)
+        return fail(PAXISIM_EINVAL, "move_cdf / move_tables / move_loop");
+      for (e = 0; e < wl->move_tables; e++)
+        for (w = 1; w + 1u < K; w++)
+          if (wl->move_cdf[e * PAXISIM_MAX_KEYS + w] < wl->move_cdf[e * PAXISIM_MAX_KEYS + w - 1])
+            return fail(PAXISIM_EINVAL, "move_cdf table %u must be non-decreasing", e);
+    }
+  }
   for (w = 0; w < wl->outstanding; w++)
     if (wl->target[w] >= N) return fail(PAXISIM_EINVAL, "target[%u]", w);
   if (fp->slow_ppm && (fp->slow_min > fp->slow_max || fp->slow_max > cfg->max_delay))
@@ -1687,6 +1756,12 @@ int oracle_create(const paxisim_config* cfg, const paxisim_workload* wl,
   s = (struct oracle_sim*)calloc(1, sizeof *s);
   if (!s) return fail(PAXISIM_ENOMEM, "oom");
   s->cfg = *cfg; s->wl = *wl; s->fp = *fp;
+  s->wl.move_cdf = NULL;                                   /* the caller's buffer is not kept */
+  if (wl->move_every) {
+    const size_t mb = (size_t)wl->move_tables * PAXISIM_MAX_KEYS * sizeof(uint32_t);
+    if (!(s->move_cdf = (uint32_t*)malloc(mb))) { free(s); return fail(PAXISIM_ENOMEM, "oom"); }
+    memcpy(s->move_cdf, wl->move_cdf, mb);
+  }
   s->N = N; s->Z = cfg->n_zones; s->W = cfg->window; s->M = cfg->mbox_cap;
   s->D = cfg->max_delay + 2u; s->NS = N + 1u;
   if (s->wl.outstanding > PAXISIM_MAX_WORKERS) s->wl.outstanding = PAXISIM_MAX_WORKERS;
@@ -1718,7 +1793,7 @@ int oracle_create(const paxisim_config* cfg, const paxisim_workload* wl,
   if (variant == PAXISIM_M2PAXOS) s->cfg.adaptive = 1;      /* m2paxos/replica.go:34-52: no -adaptive switch */
   for (z = 0, r = 0; z < s->Z; r += cfg->npz[z], z++) s->zfirst[z] = r;
   s->cl = (cluster_t*)calloc(s->C, sizeof(cluster_t));
-  if (!s->cl) { free(s); return fail(PAXISIM_ENOMEM, "oom clusters"); }
+  if (!s->cl) { free(s->move_cdf); free(s); return fail(PAXISIM_ENOMEM, "oom clusters"); }
   for (i = 0; i < s->C; i++) {
     cluster_t* c = &s->cl[i];
     entry_t* logs = (entry_t*)calloc((size_t)N * s->NK * s->W, sizeof(entry_t));
@@ -1746,6 +1821,7 @@ int oracle_destroy(oracle_sim* s) {
   uint64_t i;
   uint32_t r;
   if (!s) return 0;
+  free(s->move_cdf);
   for (i = 0; i < s->C; i++) {
     cluster_t* c = &s->cl[i];
     if (c->rep[0].inst) {

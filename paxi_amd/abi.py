@@ -6,7 +6,7 @@ structs, so the two speak exactly the same ABI.
 """
 import ctypes as C
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 MAX_N = 16
 MAX_ZONES = 16
 MAX_WORKERS = 32
@@ -94,6 +94,12 @@ class Workload(C.Structure):
         ("key_cdf", C.c_uint32 * MAX_KEYS),
         ("start_step", C.c_uint32 * MAX_WORKERS),
         ("key_min", C.c_uint32),
+        ("key_space", C.c_uint32),
+        ("key_tail", C.c_uint32),
+        ("move_every", C.c_uint32),
+        ("move_tables", C.c_uint32),
+        ("move_loop", C.c_uint32),
+        ("move_cdf", C.POINTER(C.c_uint32)),
     ]
 
 
@@ -256,7 +262,9 @@ def make_workload(outstanding=1, max_requests=0, write_ppm=1_000_000, locality_p
                   distribution="uniform", keys=None, start_step=0, key_min=0, **dist_params):
     """Closed-loop workload.  `distribution` is a Bconfig.Distribution name
     (benchmark.go:202-233, see paxi_amd.workload); the table distributions
-    ("normal", "zipfan", "exponential") need the cluster's `keys`."""
+    ("normal", "zipfan", "exponential") need the cluster's `keys`.  Other
+    options: key_space (Bconfig.K of order/uniform/conflict), move_every
+    (Bconfig.Move for normal), and the distribution's parameters."""
     from . import workload as _wl
     w = Workload()
     w.outstanding, w.max_requests, w.write_ppm, w.locality_ppm = outstanding, max_requests, write_ppm, locality_ppm

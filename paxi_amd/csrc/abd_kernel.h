@@ -41,7 +41,7 @@ __device__ __forceinline__ bool abd_majority(const Params& P, uint32_t mask) {  
 
 template <int NT>
 __device__ __forceinline__ void abd_handle_request(const Params& P, Rep<NT>& x, uint32_t cid) {  // replica.go:50-71
-  const uint32_t k = wl_key(P, x.kc, cid);
+  const uint32_t k = key_fit<NT>(P, x, wl_key(P, x.kc, cid));
   const uint32_t opid = (uint32_t)x.slot + 1u;
   x.slot = (int32_t)opid;
   const uint32_t st = x.l_c[op_i<NT>(P, x, opid, 2)] & 3u;

@@ -98,7 +98,9 @@ __device__ __forceinline__ int ep_where(const Params& P, const Rep<NT>& x, uint3
 }
 
 template <int NT>
-__device__ __forceinline__ uint32_t ep_key(const Params& P, const Rep<NT>& x, uint32_t cmd) { return wl_key(P, x.kc, cmd); }
+__device__ __forceinline__ uint32_t ep_key(const Params& P, Rep<NT>& x, uint32_t cmd) {
+  return key_fit<NT>(P, x, wl_key(P, x.kc, cmd));
+}
 
 // attributes (replica.go:58-80): seq = 1 + the largest seq among the latest
 // conflicting instance of every log (dep), and above maxSeqPerKey

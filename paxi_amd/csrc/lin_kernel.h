@@ -39,10 +39,13 @@ namespace pxs {
 
 constexpr uint32_t LIN_LW = 4;             // waves per cluster workgroup
 constexpr uint32_t LIN_SMAX = 128;         // partitions checked in LDS by the cluster kernel
+constexpr uint32_t LIN_WPL_MAX = 4;        // bit-set words per lane: up to 4096 * 4 vertices
+constexpr uint32_t LIN_VMAX = 4096u * LIN_WPL_MAX;   // larger partitions are counted as skipped
 constexpr uint16_t LIN_NOV = 0xFFFFu;      // sorted op not (yet) a vertex
-enum { LIN_ANOM = 0, LIN_OPS, LIN_BIG, LIN_NMAX, LIN_PARTS, LIN_NOUT = 8 };
+enum { LIN_ANOM = 0, LIN_OPS, LIN_BIG, LIN_NMAX, LIN_PARTS, LIN_SKIP, LIN_NOUT = 8 };
 
-// A wave's scratch for one partition of capacity cap = 64 * nw ops.
+// A wave's scratch for one partition of capacity cap = 64 * nw ops (cap <=
+// LIN_VMAX: vertex ids and DFS resume positions fit 16 bits).
 struct LinScratch {
   uint4* ops;        // [cap] sorted by start: {key | write << 31, value, start, end (refined)}
   uint16_t* vid;     // [cap] sorted index -> vertex (insertion number) or LIN_NOV
@@ -74,18 +77,83 @@ __device__ inline LinScratch lin_scratch(uint8_t* p, uint32_t nw, bool) {
 }
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+// A lane-distributed bit set of up to 4096 * WPL bits: word w lives in lane
+// w & 63, element w >> 6 of that lane's array (wave-uniform w).
+template <int WPL>
+struct LSet {
+  uint64_t m[WPL];
+  __device__ __forceinline__ static LSet zero() {
+    LSet r;
+#pragma unroll
+    for (int j = 0; j < WPL; j++) r.m[j] = 0;
+    return r;
+  }
+  __device__ __forceinline__ LSet operator&(const LSet& o) const {
+    LSet r;
+#pragma unroll
+    for (int j = 0; j < WPL; j++) r.m[j] = m[j] & o.m[j];
+    return r;
+  }
+  __device__ __forceinline__ LSet operator~() const {
+    LSet r;
+#pragma unroll
+    for (int j = 0; j < WPL; j++) r.m[j] = ~m[j];
+    return r;
+  }
+  __device__ __forceinline__ LSet& operator|=(const LSet& o) {
+#pragma unroll
+    for (int j = 0; j < WPL; j++) m[j] |= o.m[j];
+    return *this;
+  }
+  __device__ __forceinline__ bool lane_any() const {
+    uint64_t v = 0;
+#pragma unroll
+    for (int j = 0; j < WPL; j++) v |= m[j];
+    return v != 0;
+  }
+  __device__ __forceinline__ uint64_t elem(uint32_t j) const {   // m[j], j wave-uniform
+    uint64_t v = m[0];
+#pragma unroll
+    for (int k = 1; k < WPL; k++) v = j == (uint32_t)k ? m[k] : v;
+    return v;
+  }
+  // word w := v on its lane
+  __device__ __forceinline__ void put_word(uint32_t w, uint64_t v) {
+    if (lane_id() != (w & 63u)) return;
+#pragma unroll
+    for (int k = 0; k < WPL; k++)
+      if ((w >> 6) == (uint32_t)k) m[k] = v;
+  }
+};
 // word w of a lane-distributed bit set (wave-uniform w)
-__device__ __forceinline__ uint64_t mword(uint64_t m, uint32_t w) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, (int)w);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(m >> 32), (int)w);
+template <int WPL>
+__device__ __forceinline__ uint64_t mword(const LSet<WPL>& s, uint32_t w) {
+  const uint64_t m = s.elem(w >> 6);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, (int)(w & 63u));
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(m >> 32), (int)(w & 63u));
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
-__device__ __forceinline__ bool mbit(uint64_t m, uint32_t v) { return (mword(m, v >> 6) >> (v & 63u)) & 1u; }
-__device__ __forceinline__ uint64_t mset(uint64_t m, uint32_t v) {
-  return lane_id() == (v >> 6) ? m | (1ull << (v & 63u)) : m;
+template <int WPL>
+__device__ __forceinline__ bool mbit(const LSet<WPL>& s, uint32_t v) { return (mword(s, v >> 6) >> (v & 63u)) & 1u; }
+template <int WPL>
+__device__ __forceinline__ LSet<WPL> mset(LSet<WPL> s, uint32_t v) {
+  const uint32_t w = v >> 6;
+  if (lane_id() == (w & 63u)) {
+#pragma unroll
+    for (int k = 0; k < WPL; k++)
+      if ((w >> 6) == (uint32_t)k) s.m[k] |= 1ull << (v & 63u);
+  }
+  return s;
 }
-__device__ __forceinline__ uint64_t mclr(uint64_t m, uint32_t v) {
-  return lane_id() == (v >> 6) ? m & ~(1ull << (v & 63u)) : m;
+template <int WPL>
+__device__ __forceinline__ LSet<WPL> mclr(LSet<WPL> s, uint32_t v) {
+  const uint32_t w = v >> 6;
+  if (lane_id() == (w & 63u)) {
+#pragma unroll
+    for (int k = 0; k < WPL; k++)
+      if ((w >> 6) == (uint32_t)k) s.m[k] &= ~(1ull << (v & 63u));
+  }
+  return s;
 }
 __device__ __forceinline__ uint64_t or_reduce(uint64_t v) {
 #pragma unroll
@@ -93,17 +161,22 @@ __device__ __forceinline__ uint64_t or_reduce(uint64_t v) {
   return v;
 }
 __device__ __forceinline__ uint32_t first_lane(uint64_t ballot) { return (uint32_t)__builtin_ctzll(ballot); }
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l) << 32);
+}
 
 // The checker over one partition held in s.ops[0, n) (sorted).  Returns the
 // number of anomalous reads (checker.go:97: len(anomaly)).  Lanes write what
 // other lanes read next (rows, vertex fields, the DFS stack): LDS serves one
 // wave's accesses in order; with the scratch in HBM (G) a fence orders them.
-template <bool G>
+template <bool G, int WPL>
 struct LinCheck {
+  using Set = LSet<WPL>;
   LinScratch s;
   uint32_t n, nv;       // ops, vertices inserted so far
-  uint64_t present;     // lane-distributed vertex set
-  uint64_t writes;      // lane-distributed: vertices that are writes (have an input)
+  Set present;          // lane-distributed vertex set
+  Set writes;           // lane-distributed: vertices that are writes (have an input)
   __device__ __forceinline__ void sync() const {
     if (G) __threadfence_block();
   }
@@ -171,10 +244,9 @@ struct LinCheck {
   }
   // Does m reach itself?  Breadth-first over the rows, one word a lane.
   __device__ bool reaches_self(uint32_t m) const {
-    uint64_t R = mset(0ull, m), F = R;
+    Set R = mset(Set::zero(), m), F = R;
     for (;;) {
-      uint64_t nx = 0;
-      bool any = false;
+      Set nx = Set::zero();
       for (uint32_t w = 0; w < s.nw; w++) {
         uint64_t acc = 0;
         for (uint32_t b = 0; b < nv; b += 64u) {
@@ -185,11 +257,10 @@ struct LinCheck {
         }
         acc = or_reduce(acc);
         if (w == (m >> 6) && ((acc >> (m & 63u)) & 1u)) return true;
-        if (lane_id() == w) nx = acc;
+        nx.put_word(w, acc);
       }
-      nx &= present & ~R;
-      any = __ballot(nx != 0) != 0;
-      if (!any) return false;
+      nx = nx & present & ~R;
+      if (!__ballot(nx.lane_any())) return false;
       R |= nx;
       F = nx;
     }
@@ -197,9 +268,9 @@ struct LinCheck {
   // Cycle() (graph.go:212-232): DFS from each white vertex in insertion order,
   // visit (180-193) walking successors in insertion order; on a back edge the
   // gray vertices (the DFS path) are returned in `gray`.
-  __device__ bool cycle(uint64_t& gray) const {
-    uint64_t black = 0;
-    gray = 0;
+  __device__ bool cycle(Set& gray) const {
+    Set black = Set::zero();
+    gray = Set::zero();
     for (uint32_t rb = 0; rb < nv; rb += 64u) {
       uint64_t roots = mword(present & ~black, rb >> 6);
       while (roots) {
@@ -209,15 +280,24 @@ struct LinCheck {
         uint32_t sp = 0, v = root, k = 0;
         gray = mset(gray, root);
         for (;;) {
-          // the first successor u >= k of v that is not black
-          const uint32_t w = lane_id();
-          uint64_t c = 0;
-          if (w < s.nw && w * 64u + 63u >= k) {
-            c = s.rows[(size_t)v * s.nw + w] & ~black;
-            if (w * 64u < k) c &= ~0ull << (k - w * 64u);
+          // the first successor u >= k of v that is not black: word j*64 + lane
+          uint32_t u = ~0u;
+#pragma unroll
+          for (int j = 0; j < WPL; j++) {
+            const uint32_t w = (uint32_t)j * 64u + lane_id();
+            uint64_t c = 0;
+            if (w < s.nw && w * 64u + 63u >= k) {
+              c = s.rows[(size_t)v * s.nw + w] & ~black.m[j];
+              if (w * 64u < k) c &= ~0ull << (k - w * 64u);
+            }
+            const uint64_t bl = __ballot(c != 0);
+            if (bl) {
+              const uint32_t f = first_lane(bl);
+              u = ((uint32_t)j * 64u + f) * 64u + (uint32_t)__builtin_ctzll(readlane64(c, f));
+              break;
+            }
           }
-          const uint64_t bl = __ballot(c != 0);
-          if (!bl) {                                     // v done: black, back to its parent
+          if (u == ~0u) {                                // v done: black, back to its parent
             gray = mclr(gray, v);
             black = mset(black, v);
             if (sp == 0) break;
@@ -226,10 +306,6 @@ struct LinCheck {
             k = top >> 16;
             continue;
           }
-          const uint32_t f = first_lane(bl);
-          const uint64_t cw = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)c, (int)f) |
-                              ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(c >> 32), (int)f) << 32);
-          const uint32_t u = f * 64u + (uint32_t)__builtin_ctzll(cw);
           if (mbit(gray, u)) return true;
           if (lane_id() == 0) s.stk[sp] = v | ((u + 1u) << 16);
           sync();
@@ -243,7 +319,7 @@ struct LinCheck {
     return false;
   }
   // checker.go:93-100: remove the edges u->v between gray vertices with u.start > v.end
-  __device__ void cut(uint64_t gray) {
+  __device__ void cut(const Set& gray) {
     for (uint32_t b = 0; b < nv; b += 64u) {
       const uint32_t u = b + lane_id();
       const uint64_t gw = mword(gray, b >> 6);
@@ -264,7 +340,7 @@ struct LinCheck {
   // checker.linearizable (checker.go:69-104) over the sorted ops
   __device__ uint32_t run() {
     nv = 0;
-    present = writes = 0;
+    present = writes = Set::zero();
     for (uint32_t i = lane_id(); i < n; i += 64u) s.vid[i] = LIN_NOV;
     sync();
     bool maybe_cyclic = false;
@@ -279,7 +355,7 @@ struct LinCheck {
       const uint32_t m = match(o.y);
       if (m != LIN_NOV) merge(r, m);
       bool cyc = false;
-      uint64_t gray = 0;
+      Set gray;
       const bool was_cyclic = maybe_cyclic;
       if (maybe_cyclic) cyc = cycle(gray);
       else if (m != LIN_NOV && reaches_self(m)) cyc = cycle(gray);
@@ -293,7 +369,7 @@ struct LinCheck {
         if (!was_cyclic) {
           maybe_cyclic = reaches_self(m);
         } else {
-          uint64_t g2;
+          Set g2;
           maybe_cyclic = cycle(g2);
         }
       } else {
@@ -399,6 +475,10 @@ __global__ void __launch_bounds__(LIN_LW * 64) lin_cluster_kernel(Params P, uint
   for (uint32_t k = wave; k < K; k += LIN_LW) {
     const uint32_t n = koff[k + 1] - koff[k];
     if (!n) continue;
+    if (n > LIN_VMAX) {                                // beyond the bit sets: reported, not checked
+      if (lane_id() == 0) atomicAdd(&out[LIN_SKIP], 1ull);
+      continue;
+    }
     ops += n;
     if (n > LIN_SMAX) {                                // the big path
       if (lane_id() == 0) {
@@ -408,7 +488,7 @@ __global__ void __launch_bounds__(LIN_LW * 64) lin_cluster_kernel(Params P, uint
       }
       continue;
     }
-    LinCheck<false> g;
+    LinCheck<false, 1> g;
     g.s = lin_scratch(wsp, LIN_SMAX / 64u, false);
     g.n = n;
     lin_sort<false>(stage + koff[k], n, g.s);
@@ -421,13 +501,15 @@ __global__ void __launch_bounds__(LIN_LW * 64) lin_cluster_kernel(Params P, uint
 }
 
 // grid-stride over the big partitions {stage offset, ops}: one wave each,
-// scratch in HBM (slot = blockIdx.x), capacity 64 * nw ops.
+// scratch in HBM (slot = blockIdx.x), capacity 64 * nw ops; WPL bit-set words
+// per lane (nw <= 64 * WPL).
+template <int WPL>
 __global__ void __launch_bounds__(64) lin_big_kernel(const uint4* stage_all, const uint2* big, uint32_t nbig,
                                                      uint8_t* ws, uint32_t nw, unsigned long long* out) {
   const LinScratch s = lin_scratch(ws + (size_t)blockIdx.x * lin_scratch_bytes(nw, false), nw, false);
   unsigned long long anomalies = 0;
   for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
-    LinCheck<true> g;
+    LinCheck<true, WPL> g;
     g.s = s;
     g.n = big[b].y;
     lin_sort<true>(stage_all + big[b].x, g.n, g.s);

@@ -48,6 +48,7 @@ struct paxisim {
   uint32_t zone_of[PAXISIM_MAX_N], node_of[PAXISIM_MAX_N];
   std::vector<DevFault> faults;
   DevFault* d_faults = nullptr;
+  uint32_t* d_move = nullptr;      // moving-Mu key CDF tables (paxisim_workload.move_cdf)
   void* arena = nullptr;
   size_t arena_bytes = 0;
   uint64_t* d_scratch = nullptr;   // reductions
@@ -659,11 +660,49 @@ static Image proto_image(uint32_t protocol, uint32_t N, uint32_t W, uint32_t K, 
 }
 
 // The serial kernel (one wave per tile plays every replica, sim_core.h
-// sim_serial) for the protocols that have it; PAXISIM_SERIAL=0/1 overrides (A/B).
+// sim_serial) for the protocols that have it; PAXISIM_SERIAL=0/1 overrides
+// (A/B).  Any other value is refused (serial_env_ok), so an A/B arm cannot
+// silently measure the default kernel.
+static bool serial_env_ok() {
+  const char* e = getenv("PAXISIM_SERIAL");
+  return !e || !strcmp(e, "0") || !strcmp(e, "1");
+}
 static bool serial_for(uint32_t protocol) {
   const char* e = getenv("PAXISIM_SERIAL");
   (void)protocol;
-  return !e || atoi(e) != 0;
+  return !e || strcmp(e, "0") != 0;
+}
+
+// The workload's key space (paxisim.h): ORDER / UNIFORM / CONFLICT range over
+// key_space indices; CONFLICT's literal key 0 is its own index when key_min != 0.
+static uint32_t key_space_of(const paxisim_config* cfg, const paxisim_workload* wl) {
+  const uint32_t keys = cfg->keys ? cfg->keys : 1u;
+  return wl->key_space ? wl->key_space : keys;
+}
+static int check_keys(const paxisim_config* cfg, const paxisim_workload* wl) {
+  const uint32_t keys = cfg->keys ? cfg->keys : 1u;
+  const uint32_t ks = key_space_of(cfg, wl);
+  if (ks > keys) return fail(PAXISIM_EINVAL, "key_space %u exceeds keys %u", ks, keys);
+  if (wl->distribution == PAXISIM_DIST_CONFLICT && wl->key_min && ks >= keys)
+    return fail(PAXISIM_EINVAL, "conflict with key_min != 0 needs key_space < keys (literal key 0 has its own index)");
+  if (wl->distribution == PAXISIM_DIST_TABLE) {
+    for (uint32_t k = 1; k + 1u < keys; k++)
+      if (wl->key_cdf[k] < wl->key_cdf[k - 1]) return fail(PAXISIM_EINVAL, "key_cdf must be non-decreasing");
+    if (wl->key_tail && keys >= 2 && wl->key_tail < wl->key_cdf[keys - 2])
+      return fail(PAXISIM_EINVAL, "key_tail below the last key_cdf threshold");
+  } else if (wl->key_tail) {
+    return fail(PAXISIM_EINVAL, "key_tail needs a table distribution");
+  }
+  if (wl->move_every) {
+    if (wl->distribution != PAXISIM_DIST_TABLE) return fail(PAXISIM_EINVAL, "move_every needs a table distribution");
+    if (!wl->move_cdf || wl->move_tables < 1 || wl->move_loop >= wl->move_tables)
+      return fail(PAXISIM_EINVAL, "move_cdf / move_tables / move_loop");
+    for (uint32_t e = 0; e < wl->move_tables; e++)
+      for (uint32_t k = 1; k + 1u < keys; k++)
+        if (wl->move_cdf[e * PAXISIM_MAX_KEYS + k] < wl->move_cdf[e * PAXISIM_MAX_KEYS + k - 1])
+          return fail(PAXISIM_EINVAL, "move_cdf table %u must be non-decreasing", e);
+  }
+  return 0;
 }
 
 static int check_config(const paxisim_config* cfg, const paxisim_workload* wl, const paxisim_fault_process* fp,
@@ -700,16 +739,18 @@ static int check_config(const paxisim_config* cfg, const paxisim_workload* wl, c
   if (wl->outstanding > cfg->mbox_cap) return fail(PAXISIM_EINVAL, "outstanding exceeds mbox_cap");
   if (wl->distribution > PAXISIM_DIST_TABLE) return fail(PAXISIM_EINVAL, "distribution %u", wl->distribution);
   if (wl->distribution == PAXISIM_DIST_CONFLICT && wl->conflicts > 100) return fail(PAXISIM_EINVAL, "conflicts > 100");
-  if (wl->distribution == PAXISIM_DIST_TABLE)
-    for (uint32_t k = 1; k + 1u < cfg->keys; k++)
-      if (wl->key_cdf[k] < wl->key_cdf[k - 1]) return fail(PAXISIM_EINVAL, "key_cdf must be non-decreasing");
+  if (int rc = check_keys(cfg, wl)) return rc;
+  if (!serial_env_ok()) return fail(PAXISIM_EINVAL, "PAXISIM_SERIAL must be 0 or 1");
   for (uint32_t w = 0; w < wl->outstanding; w++)
     if (wl->target[w] >= N) return fail(PAXISIM_EINVAL, "target[%u]", w);
   if (fp->slow_ppm && (fp->slow_min > fp->slow_max || fp->slow_max > cfg->max_delay))
     return fail(PAXISIM_EINVAL, "slow delay range exceeds max_delay");
   const Image img = proto_image(cfg->protocol, N, cfg->window, cfg->keys, wl->outstanding, cfg->max_delay + 2u, 0);
-  // the serial kernel keeps only the image's tail (client tables on) in LDS
-  if ((serial_for(cfg->protocol) ? img.bytes - img.off_wcur + 2u * N * LANES : img.bytes) > LDS_MAX)
+  // the serial kernel keeps only the image's tail (client tables on) in LDS;
+  // either kernel adds the agreement-ring arrival counts after the image
+  const bool ring = cfg->protocol != PAXISIM_ABD && cfg->protocol != PAXISIM_EPAXOS;
+  const uint32_t agn = ring ? (2u * N * LANES + 15u) & ~15u : 0u;
+  if ((serial_for(cfg->protocol) ? img.bytes - img.off_wcur : img.bytes) + agn > LDS_MAX)
     return fail(PAXISIM_EUNSUPP, "workgroup image %u B exceeds LDS (%u B): reduce window/max_delay/replicas",
                 img.bytes, LDS_MAX);
   *N_out = N;
@@ -743,6 +784,7 @@ extern "C" int paxisim_destroy(paxisim* h) {
   flush_events(h);
   if (h->arena) (void)hipFree(h->arena);
   if (h->d_faults) (void)hipFree(h->d_faults);
+  if (h->d_move) (void)hipFree(h->d_move);
   if (h->d_scratch) (void)hipFree(h->d_scratch);
   if (h->d_cmp) (void)hipFree(h->d_cmp);
   if (h->d_pairs) (void)hipFree(h->d_pairs);
@@ -847,6 +889,13 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
   }
   if (P.variant == PAXISIM_M2PAXOS) P.adaptive = 1;
   P.key_min = wl->key_min;
+  P.kspace = key_space_of(cfg, wl);
+  P.kspace_magic = 0xFFFFFFFFu / P.kspace;
+  P.conflict_key = wl->key_min ? P.kspace : 0u;
+  P.key_tail = wl->distribution == PAXISIM_DIST_TABLE ? wl->key_tail : 0u;
+  P.move_every = wl->move_every;
+  P.move_tables = wl->move_every ? wl->move_tables : 0u;
+  P.move_loop = wl->move_every ? wl->move_loop : 0u;
   P.kv = cfg->protocol != PAXISIM_ABD && cfg->kv ? 1u : 0u;   // m2paxos/replica.go:34-52 has no -adaptive switch
   P.max_delay = cfg->max_delay;
   P.drop_ppm = fp->drop_ppm;
@@ -912,7 +961,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     // LDS stage for the first J picks of every replica's step, from what the groups leave
     uint32_t jmax = 16;
     if (const char* e = getenv("PAXISIM_STAGE")) jmax = (uint32_t)atoi(e);   // tuning override
-    const uint32_t room = (LDS_MAX / G - base) / (N * LANES * 16u);
+    const uint32_t room = LDS_MAX / G > base ? (LDS_MAX / G - base) / (N * LANES * 16u) : 0u;
     P.J = room < jmax ? room : jmax;
     if (!h->ops.staged) P.J = 0;   // that instance has no staged loop
     P.off_agn = P.img.bytes;
@@ -1003,6 +1052,14 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
       (e = hipMalloc(&h->d_faults, sizeof(DevFault) * PAXISIM_MAX_FAULTS)) != hipSuccess ||
       (e = hipMemsetAsync(h->arena, 0, zero_bytes, h->stream)) != hipSuccess)
     rc1 = fail(PAXISIM_EDEVICE, "device setup failed: %s", hipGetErrorString(e));
+  if (!rc1 && P.move_every) {   // the moving-Mu tables (the caller's buffer is not kept)
+    const size_t mb = (size_t)P.move_tables * PAXISIM_MAX_KEYS * sizeof(uint32_t);
+    if ((e = hipMalloc(&h->d_move, mb)) != hipSuccess ||
+        (e = hipMemcpy(h->d_move, wl->move_cdf, mb, hipMemcpyHostToDevice)) != hipSuccess)
+      rc1 = fail(PAXISIM_EDEVICE, "move_cdf upload failed: %s", hipGetErrorString(e));
+    P.move_cdf = h->d_move;
+  }
+  h->wl.move_cdf = nullptr;
   if (!rc1) {
     P.faults = h->d_faults;
     P.bound = h->d_cmp;
@@ -1558,9 +1615,11 @@ extern "C" int paxisim_linearizable(paxisim* h, uint64_t* anomalies, uint64_t* o
     if (bc[0]) {   // partitions above LIN_SMAX ops: one wave each, scratch in HBM
       tot[LIN_BIG] += bc[0];
       tot[LIN_NMAX] = std::max<unsigned long long>(tot[LIN_NMAX], bc[1]);
-      const uint32_t nw = (uint32_t)((bc[1] + 63u) / 64u);
-      const uint32_t waves = (uint32_t)std::min<unsigned long long>(bc[0], 2048);
-      const size_t need = (size_t)waves * lin_scratch_bytes(nw, true);
+      const uint32_t nw = (uint32_t)((bc[1] + 63u) / 64u);     // bc[1] <= LIN_VMAX (larger: skipped)
+      const size_t per = lin_scratch_bytes(nw, true);
+      const uint32_t waves = (uint32_t)std::max<unsigned long long>(
+          1, std::min<unsigned long long>(std::min<unsigned long long>(bc[0], 2048), (2ull << 30) / per));
+      const size_t need = (size_t)waves * per;
       if (need > bws_bytes) {
         (void)hipFree(bws);
         bws = nullptr;
@@ -1568,7 +1627,8 @@ extern "C" int paxisim_linearizable(paxisim* h, uint64_t* anomalies, uint64_t* o
         if ((e = hipMalloc(&bws, need)) != hipSuccess) break;
         bws_bytes = need;
       }
-      lin_big_kernel<<<waves, 64, 0, h->stream>>>(stage, big, (uint32_t)bc[0], bws, nw, out);
+      if (nw <= 64u) lin_big_kernel<1><<<waves, 64, 0, h->stream>>>(stage, big, (uint32_t)bc[0], bws, nw, out);
+      else lin_big_kernel<LIN_WPL_MAX><<<waves, 64, 0, h->stream>>>(stage, big, (uint32_t)bc[0], bws, nw, out);
       if ((e = hipGetLastError()) != hipSuccess) break;
     }
   }
@@ -1581,7 +1641,7 @@ extern "C" int paxisim_linearizable(paxisim* h, uint64_t* anomalies, uint64_t* o
   h->lin_nmax = tot[LIN_NMAX];
   if (anomalies) *anomalies = res[LIN_ANOM];
   if (ops) *ops = res[LIN_OPS];
-  if (skipped) *skipped = 0;   // no partition is too large (lin_big_kernel)
+  if (skipped) *skipped = res[LIN_SKIP];   // partitions above LIN_VMAX ops (not checked)
   return 0;
 }
 

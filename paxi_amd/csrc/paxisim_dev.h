@@ -171,7 +171,13 @@ struct Params {
   uint32_t compact;      // protocol supports compaction and it is enabled
   uint32_t variant;      // per-key protocol run by the WPaxos kernel: WPAXOS, M2PAXOS or KPAXOS
   uint32_t zfirst[PAXISIM_MAX_ZONES];   // replica index of "z.1" (KPaxos static leaders)
-  uint32_t key_min;      // Bconfig.Min: key value of key index 0
+  uint32_t key_min;      // Bconfig.Min: key value of key index 0 (ORDER / UNIFORM / CONFLICT)
+  // the workload's key space (paxisim.h paxisim_workload)
+  uint32_t kspace, kspace_magic;   // ORDER / UNIFORM / CONFLICT range over [0, kspace)
+  uint32_t conflict_key;           // index of CONFLICT's literal key 0 (kspace when key_min != 0)
+  uint32_t key_tail;               // TABLE: draws >= key_tail (nonzero) lie beyond [0, keys)
+  uint32_t move_every, move_tables, move_loop;   // moving Mu: table of command cid is (cid-1) / move_every
+  const uint32_t* move_cdf;        // [move_tables][PAXISIM_MAX_KEYS]
   // EPaxos (epaxos_kernel.h)
   uint4* ep_inst;        // [blk][r][o][W][64] x 4 uint4
   uint32_t* ep_sce;      // [3][o][r][C] slot, committed, executed

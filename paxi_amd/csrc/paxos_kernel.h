@@ -368,9 +368,9 @@ __device__ __forceinline__ void handle_request(const Params& P, Rep<NT>& x, uint
 #endif
 // (the key is computed once per executed command: kv_key)
 template <int NT>
-__device__ __forceinline__ uint32_t kv_key(const Params& P, const Rep<NT>& x, uint32_t h, uint32_t cmd) {
+__device__ __forceinline__ uint32_t kv_key(const Params& P, Rep<NT>& x, uint32_t h, uint32_t cmd) {
   // a per-key instance (HBM log: WPaxos, M2Paxos, KPaxos) only executes commands of its own key
-  return hbm_log(x) ? x.key : wl_key_h(P, h, cmd);
+  return hbm_log(x) ? x.key : key_fit<NT>(P, x, wl_key_h(P, h, cmd));
 }
 template <int NT>
 __device__ __forceinline__ uint32_t kv_get(const Params& P, Rep<NT>& x, uint32_t key) {

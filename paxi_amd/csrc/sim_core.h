@@ -314,7 +314,25 @@ __device__ __forceinline__ uint32_t mod_magic(uint32_t x, uint32_t d, uint32_t m
   uint32_t r = x - d * __umulhi(x, m);
   return r >= d ? r - d : r;
 }
-// the key of command cid given h = wl_hash(kc, cid)
+// "normal" with Bconfig.Move (benchmark.go:137-140): command cid draws from
+// the key CDF of the Mu its issue number falls in, e = (cid-1) / move_every;
+// past the last table the Mu sequence repeats from move_loop.  Upper bound by
+// binary search: the number of thresholds <= u.
+__device__ __forceinline__ uint32_t wl_key_moving(const Params& P, uint32_t u, uint32_t cid) {
+  uint32_t e = (cid - 1u) / P.move_every;
+  if (e >= P.move_tables) e = P.move_loop + (e - P.move_loop) % (P.move_tables - P.move_loop);
+  const uint32_t* t = P.move_cdf + (size_t)e * PAXISIM_MAX_KEYS;
+  uint32_t lo = 0, hi = P.keys - 1u;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (t[mid] <= u) lo = mid + 1u;
+    else hi = mid;
+  }
+  return lo;
+}
+// The key index of command cid given h = wl_hash(kc, cid): in [0, keys), or
+// keys for a table draw beyond the key space (the unbounded "exponential"
+// tail; key_fit flags it where the key is used).
 __device__ __forceinline__ uint32_t wl_key_h(const Params& P, uint32_t h, uint32_t cid) {
   if (P.locality_ppm) {
     const uint32_t w = mod_magic(cid - 1u, P.WK, P.wk_magic);        // (cid-1) % WK
@@ -322,20 +340,39 @@ __device__ __forceinline__ uint32_t wl_key_h(const Params& P, uint32_t h, uint32
     if (nk && ppm_hit(fmix32(h ^ 0x165667B1u), P.locality_ppm)) return z + P.Z * mod_magic(h, nk, P.wnk_magic[w]);
   }
   switch (P.dist) {   // Bconfig.Distribution (benchmark.go:202-233), DESIGN.md §3.8
-    case PAXISIM_DIST_ORDER: return mod_magic(cid, P.keys, P.keys_magic);
-    case PAXISIM_DIST_CONFLICT:
-      return fmix32(h ^ 0x3C6EF372u) % 100u < P.conflicts ? 0u : mod_magic(cid, P.keys, P.keys_magic);
+    case PAXISIM_DIST_ORDER: return mod_magic(cid, P.kspace, P.kspace_magic);
+    case PAXISIM_DIST_CONFLICT:   // Go's literal key 0 (benchmark.go:213-214), else the order counter + Min
+      return fmix32(h ^ 0x3C6EF372u) % 100u < P.conflicts ? P.conflict_key : mod_magic(cid, P.kspace, P.kspace_magic);
     case PAXISIM_DIST_TABLE: {   // inverse CDF; the table index is uniform, so these are scalar loads
       const uint32_t u = fmix32(h ^ 0x2545F491u);
+      if (P.move_every) return wl_key_moving(P, u, cid);
+      if (P.key_tail && u >= P.key_tail) return P.keys;
       uint32_t k = 0;
       for (uint32_t i = 0; i + 1u < P.keys; i++) k += u >= P.key_cdf[i] ? 1u : 0u;
       return k;
     }
-    default: return mod_magic(h, P.keys, P.keys_magic);
+    default: return mod_magic(h, P.kspace, P.kspace_magic);
   }
 }
 __device__ __forceinline__ uint32_t wl_key(const Params& P, uint32_t kc, uint32_t cid) {
   return wl_key_h(P, wl_hash(kc, cid), cid);
+}
+// A key the replica uses: a draw beyond the key space has no state here (Go's
+// key would be a new map entry), so the replica raises UNFAITHFUL and uses the
+// last index.
+template <int NT>
+__device__ __forceinline__ uint32_t key_fit(const Params& P, Rep<NT>& x, uint32_t k) {
+  if (k >= P.keys) {
+    x.flags |= PAXISIM_F_UNFAITHFUL;
+    k = P.keys - 1u;
+  }
+  return k;
+}
+// The key value the reference's Database sees for index k (paxisim.h)
+__device__ __forceinline__ uint32_t key_value(const Params& P, uint32_t k) {
+  if (P.dist == PAXISIM_DIST_TABLE) return k;
+  if (P.dist == PAXISIM_DIST_CONFLICT && P.key_min && k == P.conflict_key) return 0u;
+  return P.key_min + k;
 }
 __device__ __forceinline__ bool wl_write_h(const Params& P, uint32_t h) {
   return ppm_hit(fmix32(h ^ 0x27D4EB2Fu), P.write_ppm);

@@ -217,7 +217,7 @@ template <int NT>
 __device__ __forceinline__ void wp_handle_request(const Params& P, Rep<NT>& x, uint32_t req) {  // replica.go:42-66
   wp_create<NT>(P, x);                                                 // r.init(key)
   if (P.variant == PAXISIM_KPAXOS) {                                   // kpaxos/replica.go:52-62
-    const uint32_t leader = kp_leader<NT>(P, P.key_min + x.key);
+    const uint32_t leader = kp_leader<NT>(P, key_value(P, x.key));
     if (leader == x.r) paxos_handle_request<NT>(P, x, req);
     else node_forward<NT>(P, x, leader, req);                          // `go r.Forward(leader, m)`
     return;
@@ -290,7 +290,7 @@ struct WPaxosProtoT {
   template <int NT>
   __device__ static __forceinline__ void client_request(const Params& P, Rep<NT>& x, uint32_t cid) {
     PXS_CASE_T0
-    wp_bind<NT, LDS>(P, x, wl_key(P, x.kc, cid));
+    wp_bind<NT, LDS>(P, x, key_fit<NT>(P, x, wl_key(P, x.kc, cid)));
     wp_handle_request<NT>(P, x, mkreq(cid, PAXISIM_CLIENT_SRC));
     wp_unbind<NT, LDS>(P, x);
     PXS_CASE_T1(0)
@@ -309,7 +309,7 @@ struct WPaxosProtoT {
     }
     {
       PXS_CASE_T0
-      wp_bind<NT, LDS>(P, x, type == PAXISIM_MSG_REQUEST ? wl_key(P, x.kc, m.w) : hdr_key(m.x));
+      wp_bind<NT, LDS>(P, x, type == PAXISIM_MSG_REQUEST ? key_fit<NT>(P, x, wl_key(P, x.kc, m.w)) : hdr_key(m.x));
       // the entry of the message's slot (P2a / P2b / P3; harmless for the
       // others: any slot indexes the window): its load goes out with the bind's
       ecache<NT>(x, (m.z & (P.W - 1u)) * 4u);

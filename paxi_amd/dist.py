@@ -12,7 +12,8 @@ import os
 # order of the per-rank counter vector that gets all-reduced
 FLAG_NAMES = ("WOVF", "GHOST", "MBOX_OVF", "PEND_OVF", "UNFAITHFUL", "POISON", "BALLOT_OVF", "HIST_OVF")
 COUNTERS = ("delivered_total", "commits", "replies", "dropped", "client_requests", "alg_bytes",
-            "violations", "agree_compared", "agree_missed", "active") + tuple("flag_" + n for n in FLAG_NAMES)
+            "violations", "agree_compared", "agree_missed", "active", "active_start") + \
+    tuple("flag_" + n for n in FLAG_NAMES)
 
 
 def env_rank():
@@ -48,7 +49,7 @@ def reduce_counters(values, elapsed, device=None, group=None):
 
 def stats_counters(delta, alg_bytes=0, violations=0, flagged=None, **extra):
     """Counter dict from a stats delta (bench.stats_delta), scan results and
-    extra integer counters (agree_compared, agree_missed, active)."""
+    extra integer counters (agree_compared, agree_missed, active, active_start)."""
     flagged = flagged or [0] * 8
     d = {"delivered_total": delta["delivered_total"], "commits": delta["commits"], "replies": delta["replies"],
          "dropped": delta["dropped"], "client_requests": delta["client_requests"], "alg_bytes": alg_bytes,

@@ -39,6 +39,8 @@ def load_library():
     L = C.CDLL(LIB_PATH)
     abi.declare(L, "paxisim")
     L.paxisim_abi_version.restype = C.c_int
+    L.paxisim_build_id.restype = C.c_char_p
+    L.paxisim_build_id.argtypes = []
     L.paxisim_step.restype = C.c_int
     L.paxisim_step.argtypes = [C.c_void_p, C.c_uint32]
     L.paxisim_sync.restype = C.c_int
@@ -86,7 +88,12 @@ def load_library():
     return L
 
 
-EXPORTED = ["paxisim_abi_version", "paxisim_last_error", "paxisim_create", "paxisim_destroy",
+def build_id():
+    """The source fingerprint compiled into the loaded library (paxisim_build_id)."""
+    return load_library().paxisim_build_id().decode()
+
+
+EXPORTED = ["paxisim_abi_version", "paxisim_build_id", "paxisim_last_error", "paxisim_create", "paxisim_destroy",
             "paxisim_fault_add", "paxisim_step", "paxisim_sync", "paxisim_stats_get",
             "paxisim_read_state", "paxisim_read_instances", "paxisim_check", "paxisim_kernel_time", "paxisim_device_bytes",
             "paxisim_linearizable", "paxisim_history", "paxisim_occupancy", "paxisim_inject", "paxisim_read_log",

@@ -46,6 +46,7 @@ import json
 import os
 
 from . import abi, gob
+from . import workload as _wl
 
 T_REQUEST, T_REPLY, T_P1A, T_P1B, T_P1B_ENTRY, T_P2A, T_P2B, T_P3 = 1, 2, 3, 4, 5, 6, 7, 8
 T_GET, T_GETREPLY, T_SET, T_SETREPLY, T_LEADERCHG = 9, 10, 11, 12, 13
@@ -149,7 +150,8 @@ class Codec:
     def __init__(self, sim, cluster):
         self.sim, self.cluster, self.cfg = sim, cluster, sim.cfg
         self.top = Topology(sim.cfg)
-        self.key_min = sim.wl.key_min
+        self.kval = lambda k: _wl.key_value(sim.wl, sim.cfg.keys, k)     # key index <-> Command.Key
+        self.kidx = lambda v: _wl.key_index(sim.wl, sim.cfg.keys, v)
         self.proto = sim.cfg.protocol
         self._cmd = {}
 
@@ -161,7 +163,7 @@ class Codec:
 
     def command(self, cid):
         key, write = self._cmd[cid]
-        return {"Key": self.key_min + key, "Value": uvarint10(cid) if write else None, "ClientID": "",
+        return {"Key": self.kval(key), "Value": uvarint10(cid) if write else None, "ClientID": "",
                 "CommandID": cid}
 
     def check_command(self, c):
@@ -170,7 +172,7 @@ class Codec:
             raise TraceError(f"command id {cid} outside the simulator's 27 bits")
         self._commands([cid])
         key, write = self._cmd[cid]
-        if c["Key"] != self.key_min + key or (c["Value"] is not None) != write or \
+        if c["Key"] != self.kval(key) or (c["Value"] is not None) != write or \
                 (write and read_uvarint(c["Value"]) != cid):
             raise TraceError(f"command {c} is not the simulator's command {cid}")
         return cid
@@ -191,7 +193,7 @@ class Codec:
         if self.proto == abi.EPAXOS:
             return self._ep_to_go(src, t, b, s, cid, [w for r in recs[1:] for w in r[1:]])
         if self.proto == abi.ABD:
-            k = self.key_min + ((hdr >> 8) & 0xFF)
+            k = self.kval((hdr >> 8) & 0xFF)
             v = {"ID": top.id(src), "CID": b, "Key": k}
             if t in (T_GETREPLY, T_SET):                    # {opid, version, value}
                 v["Version"] = s
@@ -209,13 +211,13 @@ class Codec:
         elif t == T_P2B:
             v = {"Ballot": top.ballot64(b), "ID": top.id(src), "Slot": s}
         elif t == T_LEADERCHG and self.proto in abi.PER_KEY:
-            return KEYED_NAMES[self.proto][t], {"Key": self.key_min + key, "To": top.id(s), "From": top.id(cid),
+            return KEYED_NAMES[self.proto][t], {"Key": self.kval(key), "To": top.id(s), "From": top.id(cid),
                                                 "Ballot": top.ballot64(b)}
         else:
             raise TraceError(f"message type {t} has no Paxi wire form here")
         if self.proto in abi.PER_KEY:
             inner = {T_P1A: "P1a", T_P1B: "P1b", T_P2A: "P2a", T_P2B: "P2b", T_P3: "P3"}[t]
-            return KEYED_NAMES[self.proto][t], {"Key": self.key_min + key, inner: v}
+            return KEYED_NAMES[self.proto][t], {"Key": self.kval(key), inner: v}
         return PAXOS_NAMES[t], v
 
     # EPaxos (epaxos/msg.go:18-65): header {type | n << 8, ballot, slot, w3} + payload words
@@ -275,7 +277,7 @@ class Codec:
                 raise TraceError(f"{name} is not an EPaxos message")
             return self._ep_from_go(src, t, v)
         if t in (T_GET, T_GETREPLY, T_SET, T_SETREPLY):
-            k = v["Key"] - self.key_min
+            k = self.kidx(v["Key"])
             val = v.get("Value")
             return [(src, t | (k << 8), v["CID"], v.get("Version", 0) if t in (T_GETREPLY, T_SET) else 0,
                      read_uvarint(val) if val else 0)]
@@ -283,7 +285,7 @@ class Codec:
         if self.proto in abi.PER_KEY:
             if name not in KEYED_NAMES[self.proto].values():
                 raise TraceError(f"{name} is not a message of this protocol")
-            key = v["Key"] - self.key_min
+            key = self.kidx(v["Key"])
             if t == T_LEADERCHG:
                 return [(src, t | (key << 16), top.ballot32(v["Ballot"]), top.replica(v["To"]),
                          top.replica(v["From"]))]

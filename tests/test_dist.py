@@ -28,7 +28,8 @@ def _counters(sim):
     st = sim.stats().as_dict()
     d = {k: st[k] for k in ("delivered_total", "commits", "replies", "dropped", "client_requests")}
     return pdist.stats_counters(d, 0, sim.check(), st["flagged"], agree_compared=st["agree_compared"],
-                                agree_missed=st["agree_missed"], active=sim.cfg.clusters)
+                                agree_missed=st["agree_missed"], active=sim.cfg.clusters,
+                                active_start=sim.cfg.clusters)
 
 
 def _worker(rank, world, port, q):

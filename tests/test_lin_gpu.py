@@ -95,6 +95,39 @@ def test_large_partitions_take_the_big_path(seed):
     assert ga == oa == expect
 
 
+@pytest.mark.gpu
+def test_partitions_beyond_4096_ops():
+    """Partitions of 4097 and 5000 ops need more than one bit-set word per
+    lane (lin_big_kernel<4>): still equal to the oracle."""
+    sizes = [[4097], [5000], [300]]
+    (ga, gn, gsk), (oa, on), expect = run_case(6, sizes, N=5, H=1024)
+    assert gsk == 0 and gn == on == sum(map(sum, sizes))
+    assert ga == oa == expect
+
+
+@pytest.mark.gpu
+def test_partition_beyond_the_bit_sets_is_reported_skipped():
+    """More than 16384 ops in one (cluster, key): counted in `skipped`, its ops
+    not in `ops` (include/paxisim.h), the other partitions still checked."""
+    from paxi_amd.sim import Simulation
+    rng = random.Random(8)
+    N, H = 5, 3600
+    cfg = abi.make_config(protocol=abi.ABD, npz=[N], clusters=2, keys=2, history=H)
+    wl = abi.make_workload(outstanding=1, max_requests=1, target=[0])
+    g = Simulation(cfg, wl)
+    big, small = gen_partition(rng, 16385), gen_partition(rng, 200)
+    per = -(-len(big) // N)
+    for r in range(N):
+        ops = [(0, w, v, st, en) for (w, v, st, en) in big[r * per:(r + 1) * per]]
+        if r == 0:
+            ops += [(1, w, v, st, en) for (w, v, st, en) in small]
+        g.history_load(1, r, ops)
+    a, n, skipped = g.linearizable()
+    g.close()
+    assert skipped == 1 and n == 200
+    assert a == ol.linearizable([(v if w else None, None if w else v, s, e) for (w, v, s, e) in small])
+
+
 def tie_ops(order):
     return [tuple(o) for o in KATS["lin_tie_order"][order]]
 

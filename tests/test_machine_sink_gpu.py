@@ -1,0 +1,45 @@
+"""Guard for the MachineSink miscompile (round-3 verdict items 5 and 8,
+DESIGN.md §5.3).  Every kernel ships built with -mllvm -disable-machine-sink
+because LLVM's pre-RA MachineSink miscompiled them (a value sunk into one arm of
+a divergent branch was lost on the other arm's lanes).  build() also builds the
+two kernels that showed it WITHOUT the flag into paxi_amd/guard/libpaxisim_sink.so;
+this test runs the parity cases that caught the bug (tools/sink_guard.py) on
+that variant and on the product library, each in its own process.  Dropping the
+flag makes the product library the variant, and the product half fails.  If the
+variant half fails instead, the toolchain no longer miscompiles these cases and
+the flag can be reconsidered."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import __graft_entry__ as ge  # noqa: E402
+
+
+def test_flag_is_in_the_build():
+    assert ge.HIP_FLAGS[ge.HIP_FLAGS.index("-mllvm") + 1] == "-disable-machine-sink"
+    assert ge.GUARD_TUS and all(t in ge.HIP_SOURCES for t in ge.GUARD_TUS)
+
+
+def _run(lib):
+    env = dict(os.environ, PAXISIM_LIB=os.path.join(ROOT, lib))
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "sink_guard.py")], env=env, cwd=ROOT,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.gpu
+def test_product_library_has_no_divergence_where_the_variant_has():
+    guard = os.path.join(ROOT, ge.GUARD_LIB)
+    assert os.path.exists(guard), "guard variant not built: run __graft_entry__.build()"
+    prod = _run(ge.HIP_LIB)
+    var = _run(ge.GUARD_LIB)
+    print("product", prod, "\nvariant", var)
+    assert not any(prod["diverged"].values()), prod
+    assert any(var["diverged"].values()), f"MachineSink no longer miscompiles these cases: {var}"

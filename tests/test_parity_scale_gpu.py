@@ -22,9 +22,9 @@ pytestmark = pytest.mark.gpu
 HORIZON = {2: 25, 3: 25, 4: 25, 5: 25}
 
 
-def bench_args(cfg_id):
+def bench_args(cfg_id, fz=1):
     a = argparse.Namespace(window=None, mbox=None, kv=1, history=512, clusters=None, sim_steps=None, warmup=5,
-                           steps=20, crash_step=None)
+                           steps=20, crash_step=None, fz=fz)
     for k, v in bench.DEFAULTS[cfg_id].items():
         if getattr(a, k, None) is None:
             setattr(a, k, v)
@@ -32,10 +32,11 @@ def bench_args(cfg_id):
     return a
 
 
-@pytest.mark.parametrize("cfg_id", [2, 3, 4, 5])
-def test_sampled_parity_at_scale(cfg_id):
+@pytest.mark.parametrize("cfg_id,fz", [(2, 1), (3, 1), (4, 1), (4, 0), (5, 1)])
+def test_sampled_parity_at_scale(cfg_id, fz):
+    """fz applies to config 4: FGrid fz=1, or (fz=0) the Grid variant GridRow/GridColumn."""
     from paxi_amd.sim import Simulation
-    a = bench_args(cfg_id)
+    a = bench_args(cfg_id, fz)
     cfg, wl, fp, faults, _ = bench.workload(cfg_id, a.clusters, 0, 0, a)
     steps = HORIZON[cfg_id] * a.sim_steps
     sim = Simulation(cfg, wl, fp, faults)
@@ -45,7 +46,7 @@ def test_sampled_parity_at_scale(cfg_id):
     picks = parity_sample.choose(sim)
     res = parity_sample.check(sim, cfg, wl, fp, faults, steps, picks)
     sim.close()
-    print(f"config {cfg_id}: {res}")
+    print(f"config {cfg_id} (fz={fz}): {res}")
     assert res["compared"] >= 256
     assert res["equal"] == res["compared"], res["mismatches"]
     if cfg_id == 2:   # the timed regime: flagged and frozen clusters are in the sample

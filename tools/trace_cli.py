@@ -31,7 +31,10 @@ def to_dict(s):
     out = {}
     for name, ty in s._fields_:
         v = getattr(s, name)
-        out[name] = list(v) if isinstance(v, C.Array) else v
+        if name == "move_cdf":          # Workload's moving-Mu tables: the pointed-to thresholds
+            out[name] = [v[i] for i in range(s.move_tables * abi.MAX_KEYS)] if v else None
+        else:
+            out[name] = list(v) if isinstance(v, C.Array) else v
     return out
 
 
@@ -40,7 +43,11 @@ def from_dict(cls, d):
     for name, ty in s._fields_:
         if name not in d:
             continue
-        if issubclass(ty, C.Array):
+        if name == "move_cdf":
+            if d[name]:
+                s._move_buf = (C.c_uint32 * len(d[name]))(*d[name])
+                s.move_cdf = C.cast(s._move_buf, C.POINTER(C.c_uint32))
+        elif issubclass(ty, C.Array):
             arr = getattr(s, name)
             for i, x in enumerate(d[name]):
                 arr[i] = x

@@ -44,6 +44,7 @@ def main():
         "clusters_per_gpu": b["config"]["clusters_per_gpu"],
         "sim_steps_per_step": b["config"]["sim_steps_per_step"],
         "window": b["config"]["window"], "mbox_cap": b["config"]["mbox_cap"],
+        "fz": b["config"].get("fz", 1),
         "fetch_size_kb_per_launch": fkb,
         "write_size_kb_per_launch": wkb,
         "bytes_per_launch": (2.0 * fkb + wkb) * 1024.0,
