@@ -400,7 +400,9 @@ def main():
     if rank == 0:
         avg_launch_ms = kms / max(1, launches)
         achieved = alg_bytes(d) / max(1, launches) / (avg_launch_ms / 1e3) / 1e9   # rank 0's kernel, GB/s
-        proto = {3: "AbdProto", 5: "WPaxosProto"}.get(args.config, "PaxosProto")
+        # config 5: instance scalars in the packed HBM table (WPaxosProto), or with PAXISIM_WLDS=1 in the tile image
+        wp = "WPaxosProtoL" if os.environ.get("PAXISIM_WLDS", "0") != "0" else "WPaxosProto"
+        proto = {3: "AbdProto", 5: wp}.get(args.config, "PaxosProto")
         # the library's default step kernel is the serial one
         kname = "sim_steps" if os.environ.get("PAXISIM_SERIAL") == "0" else "sim_serial"
         occ = sim.occupancy()

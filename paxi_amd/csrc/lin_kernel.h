@@ -37,11 +37,28 @@
 
 namespace pxs {
 
+// PXS_LIN_STAMPS (diagnostic build): s_memtime cycles of the checker's phases,
+// summed over waves into out[LIN_NOUT + k] (paxisim_linearizable prints them)
+#ifdef PXS_LIN_STAMPS
+__device__ __forceinline__ uint32_t lin_now() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return (uint32_t)t;
+}
+#define LIN_T0(v) const uint32_t v = lin_now();
+#define LIN_T1(v, k) lst[k] += lin_now() - v;
+#else
+#define LIN_T0(v)
+#define LIN_T1(v, k)
+#endif
+enum { LS_P1 = 0, LS_P2, LS_SORT, LS_RUN, LS_ADD, LS_LOOK, LS_MERGE, LS_REACH };
+
 constexpr uint32_t LIN_LW = 4;             // waves per cluster workgroup
 constexpr uint32_t LIN_SMAX = 128;         // partitions checked in LDS by the cluster kernel
 constexpr uint32_t LIN_WPL_MAX = 4;        // bit-set words per lane: up to 4096 * 4 vertices
 constexpr uint32_t LIN_VMAX = 4096u * LIN_WPL_MAX;   // larger partitions are counted as skipped
 constexpr uint16_t LIN_NOV = 0xFFFFu;      // sorted op not (yet) a vertex
+constexpr uint32_t LIN_SORT_BYTES = LIN_SMAX * (16u + 4u);   // cluster kernel, per wave: sorted ops + start copies
 enum { LIN_ANOM = 0, LIN_OPS, LIN_BIG, LIN_NMAX, LIN_PARTS, LIN_SKIP, LIN_NOUT = 8 };
 
 // A wave's scratch for one partition of capacity cap = 64 * nw ops (cap <=
@@ -155,10 +172,21 @@ __device__ __forceinline__ LSet<WPL> mclr(LSet<WPL> s, uint32_t v) {
   }
   return s;
 }
+// OR over the wave's 64 lanes, uniform result.  DPP row shifts fold each row of
+// 16 lanes into its lane 15, row_bcast:15 / row_bcast:31 carry those into lane
+// 63, and one readlane broadcasts it: VALU ops only (a __shfl_xor ladder is
+// six ds_bpermute round trips through the LDS crossbar per 32-bit half).
+__device__ __forceinline__ uint32_t or_reduce32(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
 __device__ __forceinline__ uint64_t or_reduce(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
-  return v;
+  return (uint64_t)or_reduce32((uint32_t)v) | ((uint64_t)or_reduce32((uint32_t)(v >> 32)) << 32);
 }
 __device__ __forceinline__ uint32_t first_lane(uint64_t ballot) { return (uint32_t)__builtin_ctzll(ballot); }
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
@@ -380,6 +408,274 @@ struct LinCheck {
   }
 };
 
+// ---------------------------------------------------------------------------
+// LinReg: the same checker for partitions of at most 128 ops with the whole
+// graph in registers.  Lane l owns vertices l and 64 + l (slot j = v >> 6):
+// their successor rows (2 x 2 words), start, refined end and value; the sorted
+// ops are held the same way (op o at lane o & 63, slot o >> 6).  Vertex sets
+// are two wave-uniform words.  A DFS step then reads a row with four
+// readlanes and works on scalars, add / merge / remove / cut are one pass of
+// per-lane register work, and nothing touches LDS after the sort - where
+// LinCheck pays an LDS round trip per dependent access (round-4 profile:
+// lin_cluster_kernel 1.26 s for config 3's 1.68 G ops).  The semantics are
+// LinCheck's line for line (checker.go:69-104, lib/graph.go:180-232).
+// ---------------------------------------------------------------------------
+// two-word vertex set / row (v < 128): explicit fields, no dynamically indexed arrays
+struct B2 {
+  uint64_t lo, hi;
+  __device__ __forceinline__ uint64_t w(uint32_t i) const { return i ? hi : lo; }
+  __device__ __forceinline__ bool has(uint32_t v) const { return ((v >> 6 ? hi : lo) >> (v & 63u)) & 1u; }
+  // (value selects, not a selected field: a store through a selected pointer
+  // would put the owning struct in scratch memory)
+  __device__ __forceinline__ void set(uint32_t v) {
+    const uint64_t b = 1ull << (v & 63u);
+    const bool h = (v >> 6) != 0;
+    lo |= h ? 0ull : b;
+    hi |= h ? b : 0ull;
+  }
+  __device__ __forceinline__ void clr(uint32_t v) {
+    const uint64_t b = ~(1ull << (v & 63u));
+    const bool h = (v >> 6) != 0;
+    lo &= h ? ~0ull : b;
+    hi &= h ? b : ~0ull;
+  }
+  __device__ __forceinline__ bool any() const { return (lo | hi) != 0; }
+};
+__device__ __forceinline__ B2 b2(uint64_t lo, uint64_t hi) { B2 r; r.lo = lo; r.hi = hi; return r; }
+
+struct LinReg {
+  // per lane, slot j in {0, 1} (fields suffixed 0 / 1)
+  uint4 op0, op1;            // sorted op j*64+lane: {key | write << 31, value, start, end (refined)}
+  uint32_t vid0, vid1;       // sorted op -> vertex, or LIN_NOV
+  B2 row0, row1;             // successor rows of vertex j*64+lane
+  uint32_t vst0, vst1, ven0, ven1, vvl0, vvl1, opv0, opv1;
+  uint32_t stk0, stk1;       // DFS stack entry sp at lane sp & 63, slot sp >> 6
+  // wave-uniform
+  B2 present, writes;
+  uint32_t n, nv;
+#ifdef PXS_LIN_STAMPS
+  uint32_t lst[8];
+#endif
+
+  __device__ __forceinline__ static uint32_t rl(uint32_t v, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+  }
+  // slot select of a lane field; the asm barriers keep LLVM from turning the
+  // select of two fields into a load through a selected pointer (which puts
+  // the whole struct in scratch memory)
+  __device__ __forceinline__ static uint32_t pick(uint32_t i, uint32_t a0, uint32_t a1) {
+    asm volatile("" : "+v"(a0), "+v"(a1));
+    return (i >> 6) ? a1 : a0;
+  }
+  __device__ __forceinline__ static uint64_t pick64(uint32_t i, uint64_t a0, uint64_t a1) {
+    asm volatile("" : "+v"(a0), "+v"(a1));
+    return (i >> 6) ? a1 : a0;
+  }
+  __device__ __forceinline__ uint32_t op_x(uint32_t o) const { return rl(pick(o, op0.x, op1.x), o & 63u); }
+  __device__ __forceinline__ uint32_t op_y(uint32_t o) const { return rl(pick(o, op0.y, op1.y), o & 63u); }
+  __device__ __forceinline__ uint32_t op_z(uint32_t o) const { return rl(pick(o, op0.z, op1.z), o & 63u); }
+  __device__ __forceinline__ uint32_t op_w(uint32_t o) const { return rl(pick(o, op0.w, op1.w), o & 63u); }
+  __device__ __forceinline__ uint32_t vid_of(uint32_t o) const { return rl(pick(o, vid0, vid1), o & 63u); }
+  __device__ __forceinline__ uint32_t ven_of(uint32_t v) const { return rl(pick(v, ven0, ven1), v & 63u); }
+  __device__ __forceinline__ bool hb_ops(uint32_t a, uint32_t b) const { return op_w(a) < op_z(b); }   // operation.go:12-14
+  __device__ __forceinline__ uint64_t row_of(uint32_t v, uint32_t w) const {   // word w of vertex v's row
+    return readlane64(w ? pick64(v, row0.hi, row1.hi) : pick64(v, row0.lo, row1.lo), v & 63u);
+  }
+
+  // the sorted ops of the partition from the wave's LDS sort buffer
+  __device__ __forceinline__ void load(const uint4* sorted, uint32_t cnt) {
+    n = cnt;
+    nv = 0;
+    present = b2(0, 0);
+    writes = b2(0, 0);
+    const uint32_t l = lane_id();
+    op0 = l < n ? sorted[l] : make_uint4(0u, 0u, 0u, 0u);
+    op1 = l + 64u < n ? sorted[l + 64u] : make_uint4(0u, 0u, 0u, 0u);
+    vid0 = vid1 = LIN_NOV;
+    row0 = b2(0, 0);
+    row1 = b2(0, 0);
+    vst0 = vst1 = ven0 = ven1 = vvl0 = vvl1 = opv0 = opv1 = 0;
+    stk0 = stk1 = 0;
+  }
+  // checker.add (checker.go:21-33)
+  __device__ __forceinline__ void add(uint32_t o) {
+    if (vid_of(o) != LIN_NOV) return;
+    const uint32_t oz = op_z(o), ow = op_w(o), oy = op_y(o), ox = op_x(o);
+    const uint32_t id = nv++;
+    const uint32_t l = lane_id();
+    const bool own_o = l == (o & 63u), own_id = l == (id & 63u);
+    vid0 = own_o && !(o >> 6) ? id : vid0;
+    vid1 = own_o && (o >> 6) ? id : vid1;
+    const bool n0 = own_id && !(id >> 6), n1 = own_id && (id >> 6);
+    vst0 = n0 ? oz : vst0; ven0 = n0 ? ow : ven0; vvl0 = n0 ? oy : vvl0; opv0 = n0 ? o : opv0;
+    vst1 = n1 ? oz : vst1; ven1 = n1 ? ow : ven1; vvl1 = n1 ? oy : vvl1; opv1 = n1 ? o : opv1;
+    row0.lo = n0 ? 0ull : row0.lo; row0.hi = n0 ? 0ull : row0.hi;
+    row1.lo = n1 ? 0ull : row1.lo; row1.hi = n1 ? 0ull : row1.hi;
+    // v -> id for every present vertex that ended before o started (id is not yet present)
+    if (l < id && present.has(l) && ven0 < oz) row0.set(id);
+    if (l + 64u < id && present.has(l + 64u) && ven1 < oz) row1.set(id);
+    present.set(id);
+    if (ox >> 31) writes.set(id);
+  }
+  // graph.Remove (graph.go:36-48)
+  __device__ __forceinline__ void remove(uint32_t r) {
+    present.clr(r);
+    const uint32_t l = lane_id();
+    const bool z0 = l == (r & 63u) && !(r >> 6), z1 = l == (r & 63u) && (r >> 6);
+    row0.lo = z0 ? 0ull : row0.lo; row0.hi = z0 ? 0ull : row0.hi;
+    row1.lo = z1 ? 0ull : row1.lo; row1.hi = z1 ? 0ull : row1.hi;
+    row0.clr(r);
+    row1.clr(r);
+  }
+  // match (checker.go:44-52): the first write vertex in insertion order holding the value
+  __device__ __forceinline__ uint32_t match(uint32_t out) const {
+    const uint32_t l = lane_id();
+    const uint64_t m0 = __ballot(l < nv && present.has(l) && writes.has(l) && vvl0 == out);
+    if (m0) return first_lane(m0);
+    const uint64_t m1 = __ballot(l + 64u < nv && present.has(l + 64u) && writes.has(l + 64u) && vvl1 == out);
+    if (m1) return 64u + first_lane(m1);
+    return LIN_NOV;
+  }
+  // merge (checker.go:55-67)
+  __device__ __forceinline__ void merge(uint32_t r, uint32_t m) {
+    const uint32_t l = lane_id();
+    if (l < nv && l != m && row0.has(r)) row0.set(m);
+    if (l + 64u < nv && l + 64u != m && row1.has(r)) row1.set(m);
+    const uint32_t er = ven_of(r), em = ven_of(m);
+    if (er < em) {                                        // refine the merged vertex's response time
+      const uint32_t om = rl(pick(m, opv0, opv1), m & 63u);
+      ven0 = l == (m & 63u) && !(m >> 6) ? er : ven0;
+      ven1 = l == (m & 63u) && (m >> 6) ? er : ven1;
+      op0.w = l == (om & 63u) && !(om >> 6) ? er : op0.w;
+      op1.w = l == (om & 63u) && (om >> 6) ? er : op1.w;
+    }
+    remove(r);
+  }
+  // Does m reach itself?  Breadth-first over the rows of the frontier.
+  __device__ __forceinline__ bool reaches_self(uint32_t m) const {
+    const uint32_t l = lane_id();
+    B2 R = b2(0, 0);
+    R.set(m);
+    B2 F = R;
+    for (;;) {
+      uint64_t a0 = 0, a1 = 0;
+      if (F.has(l)) { a0 |= row0.lo; a1 |= row0.hi; }
+      if (F.has(l + 64u)) { a0 |= row1.lo; a1 |= row1.hi; }
+      B2 nx = b2(or_reduce(a0), or_reduce(a1));
+      if (nx.has(m)) return true;
+      nx.lo &= present.lo & ~R.lo;
+      nx.hi &= present.hi & ~R.hi;
+      if (!nx.any()) return false;
+      R.lo |= nx.lo; R.hi |= nx.hi;
+      F = nx;
+    }
+  }
+  // Cycle() (graph.go:212-232): DFS from each white vertex in insertion order,
+  // visit (180-193) walking successors in insertion order; on a back edge the
+  // gray vertices (the DFS path) are returned in `gray`.
+  __device__ __forceinline__ bool cycle(B2& gray) {
+    B2 black = b2(0, 0);
+    gray = b2(0, 0);
+    const uint32_t l = lane_id();
+    for (uint32_t rb = 0; rb < 2; rb++) {
+      uint64_t roots = present.w(rb) & ~black.w(rb);
+      while (roots) {
+        const uint32_t root = rb * 64u + (uint32_t)__builtin_ctzll(roots);
+        roots &= roots - 1u;
+        if (black.has(root)) continue;                   // reached from an earlier root
+        uint32_t sp = 0, v = root, k = 0;
+        gray.set(root);
+        for (;;) {
+          // the first successor u >= k of v that is not black
+          uint32_t u = ~0u;
+          if (k < 64u) {
+            uint64_t c = row_of(v, 0) & ~black.lo;
+            c &= ~0ull << k;
+            if (c) u = (uint32_t)__builtin_ctzll(c);
+          }
+          if (u == ~0u) {
+            uint64_t c = row_of(v, 1) & ~black.hi;
+            if (k > 64u) c &= ~0ull << (k - 64u);
+            if (c) u = 64u + (uint32_t)__builtin_ctzll(c);
+          }
+          if (u == ~0u) {                                // v done: black, back to its parent
+            gray.clr(v);
+            black.set(v);
+            if (sp == 0) break;
+            --sp;
+            const uint32_t top = rl(pick(sp, stk0, stk1), sp & 63u);
+            v = top & 0xFFFFu;
+            k = top >> 16;
+            continue;
+          }
+          if (gray.has(u)) return true;
+          const uint32_t e = v | ((u + 1u) << 16);
+          stk0 = l == (sp & 63u) && !(sp >> 6) ? e : stk0;
+          stk1 = l == (sp & 63u) && (sp >> 6) ? e : stk1;
+          sp++;
+          gray.set(u);
+          v = u;
+          k = 0;
+        }
+      }
+    }
+    return false;
+  }
+  // checker.go:93-100: remove the edges u->t between gray vertices with u.start > t.end
+  __device__ __forceinline__ void cut(const B2& gray) {
+    const uint32_t l = lane_id();
+    const bool g0 = gray.has(l), g1 = gray.has(l + 64u);
+    for (uint32_t w = 0; w < 2; w++) {
+      for (uint64_t g = gray.w(w); g; g &= g - 1u) {
+        const uint32_t t = w * 64u + (uint32_t)__builtin_ctzll(g);
+        const uint32_t et = ven_of(t);
+        if (g0 && vst0 > et) row0.clr(t);
+        if (g1 && vst1 > et) row1.clr(t);
+      }
+    }
+  }
+  // checker.linearizable (checker.go:69-104) over the sorted ops
+  __device__ __forceinline__ uint32_t run() {
+    bool maybe_cyclic = false;
+    uint32_t anomalies = 0;
+    for (uint32_t i = 0; i < n; i++) {
+      LIN_T0(ta)
+      add(i);
+      LIN_T1(ta, LS_ADD)
+      if (op_x(i) >> 31) continue;                       // a write: nothing more
+      LIN_T0(tl)
+      for (uint32_t j = i + 1; j < n && !hb_ops(i, j) && !hb_ops(j, i); j++)   // look ahead
+        if (op_x(j) >> 31) add(j);                       // concurrent writes
+      LIN_T1(tl, LS_LOOK)
+      LIN_T0(tm)
+      const uint32_t r = vid_of(i);
+      const uint32_t m = match(op_y(i));
+      if (m != LIN_NOV) merge(r, m);
+      LIN_T1(tm, LS_MERGE)
+      bool cyc = false;
+      B2 gray = b2(0, 0);
+      const bool was_cyclic = maybe_cyclic;
+      LIN_T0(tr)
+      if (maybe_cyclic) cyc = cycle(gray);
+      else if (m != LIN_NOV && reaches_self(m)) cyc = cycle(gray);
+      LIN_T1(tr, LS_REACH)
+      if (cyc) {
+        anomalies++;
+        cut(gray);
+        if (!was_cyclic) {
+          maybe_cyclic = reaches_self(m);
+        } else {
+          B2 g2;
+          maybe_cyclic = cycle(g2);
+        }
+      } else {
+        maybe_cyclic = false;
+      }
+    }
+    return anomalies;
+  }
+};
+
 // Stable sort of src[0, n) by start into s.ops (sort.Sort(byTime): ties keep
 // canonical order): each op's rank counts the ops before it.
 // The start times are first copied into the scratch's stack array (free
@@ -410,7 +706,8 @@ __device__ __forceinline__ const uint4* hist_at(const Params& P, uint64_t c, con
 
 // grid: one workgroup (LIN_LW waves) per cluster c0 + blockIdx.x.  stage:
 // [grid][N*H] ops, the cluster's history grouped by key (its own region of
-// the launch's workspace).  Dynamic LDS: LIN_LW small-partition scratches.
+// the launch's workspace).  Dynamic LDS: LIN_LW sort buffers (LIN_SORT_BYTES);
+// partitions of at most LIN_SMAX ops are checked in registers (LinReg).
 __global__ void __launch_bounds__(LIN_LW * 64) lin_cluster_kernel(Params P, uint64_t c0, uint4* stage_all,
                                                                    unsigned long long* out, uint2* big) {
   extern __shared__ uint4 lds_lin[];
@@ -422,7 +719,11 @@ __global__ void __launch_bounds__(LIN_LW * 64) lin_cluster_kernel(Params P, uint
   const uint32_t K = P.keys;
   const uint32_t cap = P.N * P.H;
   uint4* stage = stage_all + (size_t)blockIdx.x * cap;
-  uint8_t* wsp = reinterpret_cast<uint8_t*>(lds_lin) + wave * lin_scratch_bytes(LIN_SMAX / 64u, false);
+  uint8_t* wsp = reinterpret_cast<uint8_t*>(lds_lin) + wave * LIN_SORT_BYTES;
+#ifdef PXS_LIN_STAMPS
+  uint32_t lst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  LIN_T0(tp1)
   if (threadIdx.x < P.N) len[threadIdx.x] = P.execute[rc(P, threadIdx.x, c)];
   for (uint32_t k = threadIdx.x; k < LIN_LW * PAXISIM_MAX_KEYS; k += blockDim.x) (&cnt[0][0])[k] = 0;
   __syncthreads();
@@ -449,6 +750,8 @@ __global__ void __launch_bounds__(LIN_LW * 64) lin_cluster_kernel(Params P, uint
     koff[K] = acc;
   }
   __syncthreads();
+  LIN_T1(tp1, LS_P1)
+  LIN_T0(tp2)
   // pass 2: stable placement by key.  Each wave walks its slice in 64-op
   // chunks; an op goes to its key's running offset for this wave plus its
   // rank among the chunk's ops of that key (a ballot per distinct key).
@@ -470,6 +773,7 @@ __global__ void __launch_bounds__(LIN_LW * 64) lin_cluster_kernel(Params P, uint
   }
   __threadfence_block();
   __syncthreads();
+  LIN_T1(tp2, LS_P2)
   // pass 3: the keys in turn, one wave each
   unsigned long long anomalies = 0, ops = 0;
   for (uint32_t k = wave; k < K; k += LIN_LW) {
@@ -488,15 +792,32 @@ __global__ void __launch_bounds__(LIN_LW * 64) lin_cluster_kernel(Params P, uint
       }
       continue;
     }
-    LinCheck<false, 1> g;
-    g.s = lin_scratch(wsp, LIN_SMAX / 64u, false);
-    g.n = n;
-    lin_sort<false>(stage + koff[k], n, g.s);
+    LinScratch srt;                                      // the sort's LDS buffers: ops and start copies
+    srt.ops = reinterpret_cast<uint4*>(wsp);
+    srt.stk = reinterpret_cast<uint32_t*>(wsp + LIN_SMAX * 16u);
+    LIN_T0(tso)
+    lin_sort<false>(stage + koff[k], n, srt);
+    __builtin_amdgcn_wave_barrier();
+    LinReg g;
+    g.load(srt.ops, n);
+    LIN_T1(tso, LS_SORT)
+    LIN_T0(tru)
+#ifdef PXS_LIN_STAMPS
+    for (int q = 0; q < 8; q++) g.lst[q] = 0;
+#endif
     anomalies += g.run();
+    LIN_T1(tru, LS_RUN)
+#ifdef PXS_LIN_STAMPS
+    for (int q = LS_ADD; q < 8; q++) lst[q] += g.lst[q];
+#endif
+    __builtin_amdgcn_wave_barrier();                     // the next key's sort reuses the buffer
   }
   if (lane_id() == 0) {
     if (anomalies) atomicAdd(&out[LIN_ANOM], anomalies);
     if (ops) atomicAdd(&out[LIN_OPS], ops);
+#ifdef PXS_LIN_STAMPS
+    for (int q = 0; q < 8; q++) atomicAdd(&out[LIN_NOUT + q], (unsigned long long)lst[q]);
+#endif
   }
 }
 

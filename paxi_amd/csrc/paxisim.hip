@@ -254,7 +254,7 @@ __global__ void gather_inst_kernel(Params P, uint64_t lo, uint64_t n, paxisim_in
   paxisim_instance_state s;
   memset(&s, 0, sizeof s);
   if (P.protocol == PAXISIM_WPAXOS) {
-    const size_t si = (((c / LANES) * P.keys + k) * P.N + r) * LANES + (c % LANES);
+    const size_t si = wp_si(P, c / LANES, k, r, (uint32_t)(c % LANES));
     uint4 a, b;
     wp_read(P, c / LANES, k, r, (uint32_t)(c % LANES), a, b);
     s.ballot = a.x;
@@ -420,7 +420,7 @@ __global__ void read_log_kernel(Params P, uint64_t cl, uint32_t r, uint32_t key,
   uint32_t eb, ec, ea, ex;
   const uint32_t w = (uint32_t)s & (P.W - 1u);
   if (P.protocol == PAXISIM_WPAXOS) {
-    const size_t si = (((size_t)blk * P.keys + key) * P.N + r) * LANES + lane;
+    const size_t si = wp_si(P, blk, key, r, lane);
     uint4 a, b;
     wp_read(P, blk, key, r, lane, a, b);
     execute = (int32_t)a.z;
@@ -931,11 +931,15 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
   // WPaxos: the instance scalars move into the tile image when one tile's
   // image (and the agreement counts) fits the LDS; PAXISIM_WLDS=0 keeps them in HBM (A/B)
   if (P.protocol == PAXISIM_WPAXOS) {
+    // The serial kernel keeps the image in HBM, where the packed 32-B table
+    // (wst, one line per bind) moves 0.67x the bytes of the image's word
+    // planes at the same speed (A/B r4, config 5: 267 vs 400 GB per launch,
+    // profiles/r4/config5_layout.json); PAXISIM_WLDS=0/1 overrides (A/B).
     const char* ev = getenv("PAXISIM_WLDS");
     const uint32_t agn = P.AR ? (2u * N * LANES + 15u) & ~15u : 0u;
-    // (the serial kernel keeps that image region in HBM: it need not fit)
-    P.wlds = !(ev && atoi(ev) == 0) &&
-             (serial_for(P.protocol) || proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D, 1).bytes + agn <= LDS_MAX);
+    const bool ser = serial_for(P.protocol);
+    P.wlds = (ev ? atoi(ev) != 0 : !ser) &&
+             (ser || proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D, 1).bytes + agn <= LDS_MAX);
   }
   P.img = proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D, P.wlds);
   {
@@ -1602,7 +1606,7 @@ extern "C" int paxisim_linearizable(paxisim* h, uint64_t* anomalies, uint64_t* o
   if (e == hipSuccess) e = hipMalloc(&big, chunk * P.keys * sizeof(uint2));
   if (e == hipSuccess) e = hipMalloc(&out, nout * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemsetAsync(out, 0, nout * sizeof(unsigned long long), h->stream);
-  const uint32_t lds = (uint32_t)(LIN_LW * lin_scratch_bytes(LIN_SMAX / 64u, false));
+  const uint32_t lds = LIN_LW * LIN_SORT_BYTES;
   unsigned long long tot[LIN_NOUT] = {0};
   for (uint64_t c0 = 0; e == hipSuccess && c0 < P.clusters; c0 += chunk) {
     const uint64_t nc = std::min<uint64_t>(chunk, P.clusters - c0);
@@ -1632,11 +1636,17 @@ extern "C" int paxisim_linearizable(paxisim* h, uint64_t* anomalies, uint64_t* o
       if ((e = hipGetLastError()) != hipSuccess) break;
     }
   }
-  uint64_t res[LIN_NOUT] = {0};
+  uint64_t res[LIN_NOUT + 8] = {0};
   if (e == hipSuccess) e = hipMemcpyAsync(res, out, sizeof res, hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   cleanup();
   if (e != hipSuccess) return fail(PAXISIM_EDEVICE, "linearizable: %s", hipGetErrorString(e));
+#ifdef PXS_LIN_STAMPS
+  fprintf(stderr, "lin stamps (wave-cycles): p1 %llu p2 %llu sort %llu run %llu | add %llu look %llu merge %llu reach %llu\n",
+          (unsigned long long)res[LIN_NOUT + 0], (unsigned long long)res[LIN_NOUT + 1], (unsigned long long)res[LIN_NOUT + 2],
+          (unsigned long long)res[LIN_NOUT + 3], (unsigned long long)res[LIN_NOUT + 4], (unsigned long long)res[LIN_NOUT + 5],
+          (unsigned long long)res[LIN_NOUT + 6], (unsigned long long)res[LIN_NOUT + 7]);
+#endif
   h->lin_big = tot[LIN_BIG];
   h->lin_nmax = tot[LIN_NMAX];
   if (anomalies) *anomalies = res[LIN_ANOM];

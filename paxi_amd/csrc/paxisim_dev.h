@@ -197,7 +197,15 @@ struct Params {
 // [(k*N + r)*5 + word][lane] = {ballot, slot, execute, meta | npend << 4,
 // policy | committed window << 16}, and the digest in wdig.
 constexpr uint32_t WP_WORDS = 5;
+// Instance index of (blk, key k, replica r, lane) in the per-instance HBM
+// arrays (wst, wdig, wlog, wpend, wpx).  Key-major keeps one key's 64 lanes
+// together; lane-major (PXS_WP_LANEMAJOR) keeps one lane's K instances
+// together, so the instances a replica-step binds share few lines.
+#ifndef PXS_WP_LANEMAJOR
+#define PXS_WP_LANEMAJOR 0
+#endif
 __device__ __forceinline__ size_t wp_si(const Params& P, uint64_t blk, uint32_t k, uint32_t r, uint32_t lane) {
+  if (PXS_WP_LANEMAJOR) return ((blk * P.N + r) * 64u + lane) * P.keys + k;
   return ((blk * P.keys + k) * P.N + r) * 64u + lane;
 }
 __device__ __forceinline__ uint32_t* wp_img(const Params& P, uint64_t blk, uint32_t k, uint32_t r, uint32_t lane) {

@@ -395,7 +395,7 @@ __device__ __forceinline__ void kv_exec(const Params& P, Rep<NT>& x, uint32_t h,
 template <int NT>
 __device__ __forceinline__ void digest_need(const Params& P, Rep<NT>& x) {
   if (hbm_log(x) && P.wlds && x.dig_st == 0u) {
-    x.digest = P.wdig[(((size_t)x.blk * P.keys + x.key) * nrep<NT>(P) + x.r) * LANES + x.lane];
+    x.digest = P.wdig[wp_si(P, x.blk, x.key, x.r, x.lane)];
     x.dig_st = 1u;
   }
 }

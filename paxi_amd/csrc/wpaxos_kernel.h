@@ -35,6 +35,7 @@ namespace pxs {
 
 template <int NT>
 __device__ __forceinline__ size_t wp_slot(const Params& P, const Rep<NT>& x, uint32_t key) {
+  if (PXS_WP_LANEMAJOR) return (((size_t)x.blk * nrep<NT>(P) + x.r) * LANES + x.lane) * P.keys + key;
   return (((size_t)x.blk * P.keys + key) * nrep<NT>(P) + x.r) * LANES + x.lane;
 }
 
