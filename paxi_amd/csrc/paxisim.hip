@@ -49,6 +49,7 @@ struct paxisim {
   std::vector<DevFault> faults;
   DevFault* d_faults = nullptr;
   uint32_t* d_move = nullptr;      // moving-Mu key CDF tables (paxisim_workload.move_cdf)
+  uint32_t* d_ph = nullptr;        // phase binning: class counts, region, per-block sums
   void* arena = nullptr;
   size_t arena_bytes = 0;
   uint64_t* d_scratch = nullptr;   // reductions
@@ -509,6 +510,7 @@ __device__ void swap_slots(const Params& P, uint64_t p, uint64_t q, uint32_t j) 
   swap_rows(P.wrep, P.WK, C, p, q, j);
   swap_rows(P.frz, 1, C, p, q, j);
   swap_rows(P.qf, 1, C, p, q, j);
+  if (P.phase_sort) swap_rows(P.phase, 1, C, p, q, j);
   swap_lanes(P.reqx, (size_t)N * P.W * LANES, (size_t)N * P.W, p, q, j);
   // LDS image: u32 rows (log window a/b/c, worker tables, poison), then u8 mailbox counts
   swap_lanes(reinterpret_cast<uint32_t*>(P.image), P.img.bytes / 4u, P.img.off_cnt / (LANES * 4u), p, q, j);
@@ -619,6 +621,92 @@ __global__ void cmp_freeze(Params P, uint32_t* cm, uint32_t t) {
 __global__ void cmp_setbound(uint32_t* cm) { cm[CM_BOUND] = cm[CM_LNEW]; }
 
 __global__ void swap_one(Params P, uint64_t p, uint64_t q) { swap_slots(P, p, q, threadIdx.x); }
+
+// ---------------------------------------------------------------------------
+// Phase binning.  After the live/dead partition, the stepped
+// slots [0, bound) are grouped by class - the phase residue each live cluster
+// was busiest at in the last launch, then the quiescent slots - with the same
+// pair swaps: pass p moves every class-p slot into the region [base_p, end_p)
+// by swapping the k-th misplaced slot inside it with the k-th class-p slot
+// beyond it.  Slots that kept their phase stay where they are, so a pass costs
+// the clusters whose phase drifted.
+// ---------------------------------------------------------------------------
+enum { PH_N = 0, PH_BASE = 8, PH_END = 9, PH_SUMS = 16 };   // PH_N + class: classes 0..period (quiescent last)
+__device__ __forceinline__ uint32_t ph_class(const Params& P, uint64_t s) {
+  return P.qf[s] ? P.phase_period : P.phase[s];
+}
+__global__ void ph_classes(Params P, const uint32_t* cm, uint32_t* ph) {
+  const uint64_t s = (uint64_t)blockIdx.x * CB + threadIdx.x;
+  const uint32_t bound = cm[CM_BOUND];
+  const uint32_t c = s < bound ? ph_class(P, s) : 0xFFu;
+  for (uint32_t k = 0; k <= P.phase_period; k++) {
+    const int n = __syncthreads_count(c == k);
+    if (threadIdx.x == 0 && n) atomicAdd(&ph[PH_N + k], (uint32_t)n);
+  }
+}
+// region of class p: [sum of classes < p, + count of p)
+__global__ void ph_region(uint32_t* ph, uint32_t p) {
+  uint32_t b = 0;
+  for (uint32_t k = 0; k < p; k++) b += ph[PH_N + k];
+  ph[PH_BASE] = b;
+  ph[PH_END] = b + ph[PH_N + p];
+}
+// per block: misplaced slots inside the region (class != p) and class-p slots beyond it
+__global__ void ph_count(Params P, const uint32_t* cm, uint32_t* ph, uint32_t p, uint32_t nb) {
+  const uint64_t s = (uint64_t)blockIdx.x * CB + threadIdx.x;
+  const uint32_t bound = cm[CM_BOUND], base = ph[PH_BASE], end = ph[PH_END];
+  const uint32_t c = s < bound ? ph_class(P, s) : 0xFFu;
+  const int in = __syncthreads_count(s >= base && s < end && c != p);
+  const int out = __syncthreads_count(s >= end && s < bound && c == p);
+  if (threadIdx.x == 0) {
+    ph[PH_SUMS + blockIdx.x] = (uint32_t)in;
+    ph[PH_SUMS + nb + blockIdx.x] = (uint32_t)out;
+  }
+}
+// exclusive scans of both count arrays (one workgroup); the pair count to cm
+__global__ void ph_scan(uint32_t* cm, uint32_t* ph, uint32_t nb) {
+  __shared__ uint32_t sh[CB];
+  __shared__ uint32_t carry;
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t a = 0; a < 2; a++) {
+    uint32_t* arr = ph + PH_SUMS + a * nb;
+    if (tid == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < nb; base += CB) {
+      const uint32_t v = base + tid < nb ? arr[base + tid] : 0u;
+      sh[tid] = v;
+      __syncthreads();
+      for (uint32_t off = 1; off < CB; off <<= 1) {
+        const uint32_t t = tid >= off ? sh[tid - off] : 0u;
+        __syncthreads();
+        sh[tid] += t;
+        __syncthreads();
+      }
+      if (base + tid < nb) arr[base + tid] = carry + sh[tid] - v;
+      __syncthreads();
+      if (tid == 0) carry += sh[CB - 1];
+      __syncthreads();
+    }
+    if (a == 0 && tid == 0) cm[CM_NPAIRS] = carry;   // misplaced inside = class-p outside
+  }
+}
+__global__ void ph_index(Params P, const uint32_t* cm, const uint32_t* ph, uint32_t p, uint32_t nb, uint32_t* lo,
+                         uint32_t* hi) {
+  __shared__ uint32_t wa[CB / LANES], wb[CB / LANES];
+  const uint64_t s = (uint64_t)blockIdx.x * CB + threadIdx.x;
+  const uint32_t bound = cm[CM_BOUND], base = ph[PH_BASE], end = ph[PH_END];
+  const uint32_t c = s < bound ? ph_class(P, s) : 0xFFu;
+  const bool in = s >= base && s < end && c != p, out = s >= end && s < bound && c == p;
+  const uint64_t ma = __ballot(in), mb = __ballot(out);
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  if (lane == 0) { wa[w] = (uint32_t)__popcll(ma); wb[w] = (uint32_t)__popcll(mb); }
+  __syncthreads();
+  uint32_t oa = 0, ob = 0;
+  for (uint32_t k = 0; k < w; k++) { oa += wa[k]; ob += wb[k]; }
+  const uint64_t below = (1ull << lane) - 1ull;
+  if (in) lo[ph[PH_SUMS + blockIdx.x] + oa + (uint32_t)__popcll(ma & below)] = (uint32_t)s;
+  if (out) hi[ph[PH_SUMS + nb + blockIdx.x] + ob + (uint32_t)__popcll(mb & below)] = (uint32_t)s;
+}
 
 // Wake: the link fault process of slots [s0, s1) over the steps they were frozen
 __global__ void replay_kernel(Params P, uint64_t s0, uint64_t s1, uint32_t tnow) {
@@ -785,6 +873,7 @@ extern "C" int paxisim_destroy(paxisim* h) {
   if (h->arena) (void)hipFree(h->arena);
   if (h->d_faults) (void)hipFree(h->d_faults);
   if (h->d_move) (void)hipFree(h->d_move);
+  if (h->d_ph) (void)hipFree(h->d_ph);
   if (h->d_scratch) (void)hipFree(h->d_scratch);
   if (h->d_cmp) (void)hipFree(h->d_cmp);
   if (h->d_pairs) (void)hipFree(h->d_pairs);
@@ -980,6 +1069,17 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
         P.off_wscr = base;
         P.lds_bytes += P.keys * WP_WORDS * LANES * 4u;
       }
+      // phase binning (Paxos, with compaction): per-residue record counts after the rest
+      const char* pe = getenv("PAXISIM_PHASE_SORT");
+      const char* pp = getenv("PAXISIM_PHASE_PERIOD");
+      const char* ce = getenv("PAXISIM_COMPACT");
+      if (P.protocol == PAXISIM_PAXOS && !(ce && atoi(ce) == 0) && (pe ? atoi(pe) != 0 : PXS_PHASE_SORT)) {
+        P.phase_period = pp ? (uint32_t)atoi(pp) : 3u;
+        if (P.phase_period < 2u || P.phase_period > 7u) { delete h; return fail(PAXISIM_EINVAL, "PAXISIM_PHASE_PERIOD in [2,7]"); }
+        P.ph_rel = P.lds_tail + P.lds_bytes - P.img.off_cnt;
+        P.lds_bytes += P.phase_period * LANES * 4u;
+        P.phase_sort = 1;
+      }
     }
   }
   P.C = (cfg->clusters + LANES * P.G - 1) / (LANES * P.G) * (LANES * P.G);
@@ -1007,6 +1107,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     uint4* wpx = carve<uint4>(p, wp && cfg->policy != PAXISIM_POLICY_CONSECUTIVE ? NIC * 3 : 0);
     uint4* hist = carve<uint4>(p, NC * P.H);
     uint32_t* maps = carve<uint32_t>(p, C * 4);
+    uint32_t* phs = carve<uint32_t>(p, C);
     unsigned long long* agr = carve<unsigned long long>(p, (size_t)P.AR * P.NK * C);
     uint4* agq = carve<uint4>(p, P.AR ? (size_t)2 * AGMAX * N * C : 0);
     const bool ep = P.protocol == PAXISIM_EPAXOS;
@@ -1028,6 +1129,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
       P.ck_e = cke; P.ck_d = ckd; P.stats = st; P.reqx = reqx; P.hist = hist; P.image = image; P.rec = rec;
       P.wst = wst; P.wdig = wdig; P.wlog = wlog; P.wpend = wpend; P.gst = gst; P.wpx = wpx;
       P.slot_of = maps; P.cl_of = maps + C; P.frz = maps + 2 * C; P.qf = maps + 3 * C;
+      P.phase = phs;
       P.agr = agr;
       P.agq = agq;
       P.ep_inst = ep_inst; P.ep_sce = ep_sce; P.ep_cf = ep_cf; P.ep_max = ep_max;
@@ -1053,6 +1155,7 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
       (e = hipMalloc(&h->d_scratch, sizeof(uint64_t) * 64)) != hipSuccess ||
       (e = hipMalloc(&h->d_cmp, sizeof(uint32_t) * ncmp)) != hipSuccess ||
       (e = hipMalloc(&h->d_pairs, sizeof(uint32_t) * 2 * (C / 2 + LANES))) != hipSuccess ||
+      (e = hipMalloc(&h->d_ph, sizeof(uint32_t) * (PH_SUMS + 2 * ((cfg->clusters + CB - 1) / CB)))) != hipSuccess ||
       (e = hipMalloc(&h->d_faults, sizeof(DevFault) * PAXISIM_MAX_FAULTS)) != hipSuccess ||
       (e = hipMemsetAsync(h->arena, 0, zero_bytes, h->stream)) != hipSuccess)
     rc1 = fail(PAXISIM_EDEVICE, "device setup failed: %s", hipGetErrorString(e));
@@ -1125,6 +1228,18 @@ static int compact(paxisim* h) {
   cmp_swap<<<4096, LANES, 0, h->stream>>>(P, h->d_cmp, lo, hi);
   cmp_freeze<<<nb, CB, 0, h->stream>>>(P, h->d_cmp, h->t);
   cmp_setbound<<<1, 1, 0, h->stream>>>(h->d_cmp);
+  if (P.phase_sort) {   // group the stepped slots by phase class
+    uint32_t* ph = h->d_ph;
+    HIPCHK(hipMemsetAsync(ph, 0, PH_SUMS * sizeof(uint32_t), h->stream));
+    ph_classes<<<nb, CB, 0, h->stream>>>(P, h->d_cmp, ph);
+    for (uint32_t p = 0; p < P.phase_period; p++) {   // classes 0..period-1; the quiescent ones end up last
+      ph_region<<<1, 1, 0, h->stream>>>(ph, p);
+      ph_count<<<nb, CB, 0, h->stream>>>(P, h->d_cmp, ph, p, nb);
+      ph_scan<<<1, CB, 0, h->stream>>>(h->d_cmp, ph, nb);
+      ph_index<<<nb, CB, 0, h->stream>>>(P, h->d_cmp, ph, p, nb, lo, hi);
+      cmp_swap<<<4096, LANES, 0, h->stream>>>(P, h->d_cmp, lo, hi);
+    }
+  }
   HIPCHK(hipGetLastError());
   h->last_cmp = h->t;
   return 0;

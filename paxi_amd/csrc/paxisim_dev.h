@@ -169,6 +169,12 @@ struct Params {
   uint32_t* qf;          // [C] per slot
   uint32_t* bound;       // device scalar: slots [0, *bound) are stepped
   uint32_t compact;      // protocol supports compaction and it is enabled
+  // Phase binning (serial kernel): each launch sums the records a
+  // cluster's replicas handle per (step mod phase_period) in LDS (at l_cnt +
+  // ph_rel), and ends by writing the busiest residue to phase[slot]; compaction
+  // then groups live clusters by it, so a wave's lanes have their bursts together.
+  uint32_t phase_sort, phase_period, ph_rel;
+  uint32_t* phase;       // [C] per slot
   uint32_t variant;      // per-key protocol run by the WPaxos kernel: WPAXOS, M2PAXOS or KPAXOS
   uint32_t zfirst[PAXISIM_MAX_ZONES];   // replica index of "z.1" (KPaxos static leaders)
   uint32_t key_min;      // Bconfig.Min: key value of key index 0 (ORDER / UNIFORM / CONFLICT)
@@ -403,6 +409,12 @@ __device__ __forceinline__ void stamp_case(const Params& P, uint32_t blk, uint32
 // in tiles per CU (8 -> 5 on config 5) than it saves (A/B r3: -35%).
 #ifndef PXS_WP_SCRATCH
 #define PXS_WP_SCRATCH 0
+#endif
+
+// Phase binning of live clusters at compaction; the default,
+// overridden at run time by PAXISIM_PHASE_SORT=0/1
+#ifndef PXS_PHASE_SORT
+#define PXS_PHASE_SORT 0
 #endif
 
 // ---- SoA addressing --------------------------------------------------------

@@ -611,6 +611,8 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
       total += n;
     }
   }
+  if (P.phase_sort)   // this step's load of the cluster, by step residue (serial kernel)
+    reinterpret_cast<uint32_t*>(x.l_cnt + P.ph_rel)[((x.t % P.phase_period) << 6) | x.lane] += total;
 
   // merge order: weighted pick among sources, two 16-bit picks per draw;
   // the next message's record is loaded before the current one is handled
@@ -1159,6 +1161,8 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
   x.rec = P.rec + (size_t)blk * P.rec_per_block;
   if (P.AR)
     for (uint32_t k = x.lane; k < 2u * N * LANES; k += LANES) x.l_agn[k] = 0;
+  if (P.phase_sort)
+    for (uint32_t k = 0; k < P.phase_period; k++) reinterpret_cast<uint32_t*>(x.l_cnt + P.ph_rel)[(k << 6) | x.lane] = 0;
   const bool live = x.c < bound;
   x.es = Proto::kind == PAXISIM_WPAXOS ? 4u : LANES;
   x.hw = true;   // every window is in the HBM image here
@@ -1214,6 +1218,15 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
     const uint32_t nbox = P.D * N * (N + 1u);
     for (uint32_t b = 0; b < nbox; b++) any |= x.l_cnt[(b << 6) | x.lane];
     P.qf[x.c] = any ? 0u : 1u;
+    if (P.phase_sort) {   // the residue with the most records (the first on ties)
+      const uint32_t* ph = reinterpret_cast<const uint32_t*>(x.l_cnt + P.ph_rel);
+      uint32_t best = 0, most = ph[x.lane];
+      for (uint32_t k = 1; k < P.phase_period; k++) {
+        const uint32_t v = ph[(k << 6) | x.lane];
+        if (v > most) { most = v; best = k; }
+      }
+      P.phase[x.c] = best;
+    }
   }
   {
     const uint32_t nb = (P.img.bytes - tail) / 16u;

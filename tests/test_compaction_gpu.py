@@ -87,3 +87,31 @@ def test_compaction_on_equals_off(monkeypatch):
         s.close()
     assert res[0][:3] == res[1][:3]
     assert res[0][3] < res[1][3] == cfg.clusters
+
+
+@pytest.mark.parametrize("period", ["3", "2"])
+def test_phase_binning_is_invisible(monkeypatch, period):
+    """Phase binning reorders every live cluster's slot at each
+    compaction by the step residue it was busiest at; the state is bit-exact
+    with the oracle, and with compaction off, including the wake path."""
+    monkeypatch.setenv("PAXISIM_PHASE_SORT", "1")
+    monkeypatch.setenv("PAXISIM_PHASE_PERIOD", period)
+    monkeypatch.setenv("PAXISIM_COMPACT_EVERY", "20")
+    cfg = abi.make_config(npz=[5], clusters=2048 + 37, seed=9, window=16, mbox_cap=32, max_delay=4,
+                          steps_per_launch=10)
+    wl = abi.make_workload(outstanding=8, target=0)
+    fp = abi.make_fault_process(drop_ppm=3000, drop_len=40, slow_ppm=3000, slow_len=30, slow_min=1, slow_max=4)
+    g, o = _pair(cfg, wl, fp)
+    for k in range(6):
+        g.step(70)
+        o.step(70)
+        assert_same(g, o, f"chunk {k}")
+    cid = 1 << 22
+    for c in range(0, cfg.clusters, 41):                   # wake frozen clusters too
+        g.inject(c, 0, cid)
+        o.inject(c, 0, cid)
+        cid += 1
+    g.step(60)
+    o.step(60)
+    assert_same(g, o, "after wake")
+    _logs_same(g, o, range(0, cfg.clusters, 97), 5)

@@ -1,0 +1,91 @@
+"""Lane imbalance of the serial step kernel, and what re-binning clusters into
+waves could recover (round-3 verdict item 3), measured offline on the oracle.
+
+A wave of the serial kernel runs replica r's replica-step for its 64 clusters
+together, so each (step, replica) costs about as many merge trips as its
+busiest lane needs.  This runs a BASELINE config's clusters on the CPU oracle
+from step `start` for `steps` steps, takes the exact number of records every
+(cluster, replica) handles at every step, and prices assignments of the live
+clusters to waves of 64 by cost = sum over steps, replicas and waves of the
+largest lane count, against the mean (sum / 64):
+  random       - the order compaction leaves (no re-binning)
+  load         - sorted by the previous half-window's message count (the proxy
+                 the verdict names: last launch's delivered count)
+  phase k      - sorted by the convoy phase: the step (mod k) at which the
+                 cluster's leader was busiest in the previous half-window
+  phase k (same window) - the same, measured on the priced window itself (a bound)
+The oracle is the checker here, not the thing measured.
+usage: python tools/imbalance.py <config> <clusters> <start> <steps> [out.json]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import bench  # noqa: E402
+import oracle_lib as ol  # noqa: E402
+
+
+def counts(cfg_id, C, start, T):
+    a = argparse.Namespace(window=None, mbox=None, kv=1, history=512, clusters=C, sim_steps=None, warmup=5,
+                           steps=20, crash_step=None, fz=1)
+    for k, v in bench.DEFAULTS[cfg_id].items():
+        if getattr(a, k, None) is None:
+            setattr(a, k, v)
+    a.crash_step = a.warmup * a.sim_steps
+    cfg, wl, fp, faults, _ = bench.workload(cfg_id, C, 0, 0, a)
+    o = ol.OracleSim(cfg, wl, fp, faults)
+    o.step(start, threads=min(8, os.cpu_count() or 1))
+    N = sum(cfg.npz[i] for i in range(cfg.n_zones))
+
+    def deliv():
+        return np.array([sum(s.delivered) + s.client_requests for s in o.read_state()]).reshape(C, N)
+    prev, M = deliv(), np.zeros((T, C, N), dtype=np.int32)
+    for t in range(T):
+        o.step(1)
+        cur = deliv()
+        M[t], prev = cur - prev, cur
+    o.close()
+    return M
+
+
+def main():
+    cfg_id, C, start, T = (int(x) for x in sys.argv[1:5])
+    M = counts(cfg_id, C, start, T)
+    live = M.sum(axis=(0, 2)) > 0
+    Ml = M[:, live, :]
+    L = Ml.shape[1] // 64 * 64
+    Ml = Ml[:, :L, :]
+    h = T // 2
+    rng = np.random.default_rng(0)
+
+    def cost(perm, lo, hi):
+        X = Ml[lo:hi][:, perm, :].reshape(hi - lo, L // 64, 64, -1)
+        return float(X.max(axis=2).sum() / (Ml[lo:hi].sum() / 64.0))
+
+    res = {"config": cfg_id, "clusters": C, "live": int(L), "window": [start, start + T],
+           "metric": "sum over steps, replicas and waves of the largest lane's records / the mean lane's (1 = no imbalance)",
+           "priced_on": [start + h, start + T]}
+    res["random"] = cost(rng.permutation(L), h, T)
+    res["load"] = cost(np.argsort(Ml[:h].sum(axis=(0, 2)), kind="stable"), h, T)
+    lead = Ml[:, :, :].sum(axis=2) if cfg_id == 5 else Ml[:, :, 0]
+    for k in (2, 3, 4, 6):
+        for name, (lo, hi) in (("phase%d" % k, (0, h)), ("phase%d_same_window" % k, (h, T))):
+            ph = np.zeros((L, k))
+            for t in range(lo, hi):
+                ph[:, (start + t) % k] += lead[t]
+            res[name] = cost(np.lexsort((ph.sum(axis=1), np.argmax(ph, axis=1))), h, T)
+    x = lead.astype(float) - lead.mean(axis=0)
+    res["leader_autocorrelation"] = {str(g): float((x[g:] * x[:-g]).sum() / (x * x).sum()) for g in range(1, 7)}
+    out = json.dumps(res, indent=1)
+    print(out)
+    if len(sys.argv) > 5:
+        open(sys.argv[5], "w").write(out + "\n")
+
+
+if __name__ == "__main__":
+    main()
