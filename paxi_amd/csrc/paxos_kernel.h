@@ -52,6 +52,7 @@ __device__ __forceinline__ uint32_t eb(Rep<NT>& x, uint32_t i) {
 template <int NT>
 __device__ __forceinline__ uint32_t ec(Rep<NT>& x, uint32_t i) {
   if (hbm_log(x)) { ecache(x, i); return x.ce.z; }
+  if (wb_on(x) && x.ci == i) return x.ce.z;
   return x.l_c[i];
 }
 template <int NT>
@@ -74,6 +75,12 @@ __device__ __forceinline__ void set_b(Rep<NT>& x, uint32_t i, uint32_t v) {
 template <int NT>
 __device__ __forceinline__ void set_c(Rep<NT>& x, uint32_t i, uint32_t v) {
   if (hbm_log(x)) { x.l_a[i + 2u] = v; if (x.ci == i) x.ce.z = v; return; }
+  if (wb_on(x)) {
+    if (x.ci != i) wb_flush(x);
+    x.ci = i;
+    x.ce.z = v;
+    return;
+  }
   x.l_c[i] = v;
 }
 template <int NT>
@@ -88,6 +95,7 @@ __device__ __forceinline__ void eput(Rep<NT>& x, uint32_t i, const Ent& e) {
     cm_note(x, i, e.c);
     return;
   }
+  if (wb_on(x) && x.ci == i) x.ci = ~0u;            // superseded by this write
   x.l_a[i] = e.b;
   x.l_b[i] = e.c;
   x.l_c[i] = e.a;

@@ -1087,6 +1087,24 @@ __global__ void __launch_bounds__(max_threads<NT>(), min_waves<NT>()) sim_steps(
 // the HBM image), so many more tiles are resident per CU.  The replica's
 // registers are loaded from and stored to HBM around each replica-step.
 // ---------------------------------------------------------------------------
+// PXS_WB_ACK: with the three planes in HBM (the serial Multi-Paxos kernel) the
+// ack word a P2b writes is held back in (ci, ce.z) and stored after the next
+// trip's entry loads have issued, so their waits do not include it (vmcnt
+// retires loads and stores in issue order).  Every reader of plane c goes
+// through ec(), a direct write of index ci drops the pending one, and each
+// replica-step ends with wb_flush (paxos_kernel.h set_c / eput).
+#ifndef PXS_WB_ACK
+#define PXS_WB_ACK 0
+#endif
+template <int NT>
+__device__ __forceinline__ bool wb_on(const Rep<NT>& x) { return PXS_WB_ACK && x.hw && x.es != 4u; }
+template <int NT>
+__device__ __forceinline__ void wb_flush(Rep<NT>& x) {
+  if (wb_on(x) && x.ci != ~0u) {
+    x.l_c[x.ci] = x.ce.z;
+    x.ci = ~0u;
+  }
+}
 #ifndef PXS_SERIAL_WAVES
 #define PXS_SERIAL_WAVES 2   // waves per SIMD the register budget must allow (2: <= 256 VGPRs; A/B r3: 3 waves at 168 VGPRs spill 127 and run 10-24% slower)
 #endif
@@ -1203,6 +1221,7 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
 #else
         replica_step<NT, Proto, false>(P, x);
 #endif
+        wb_flush<NT>(x);
         P.flags[i] = x.flags;
         if (P.kv) P.kv_ver[i] = x.kvver;
         Proto::template store<NT>(P, x);

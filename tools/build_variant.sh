@@ -19,5 +19,5 @@ for p in "${pids[@]}"; do wait "$p"; done
 VID="$(python3 -c "import __graft_entry__ as g; print(g.source_id())")+$(echo "$@" | md5sum | cut -c1-8)"
 printf 'extern "C" const char* paxisim_build_id(void) { return "%s"; }\n' "$VID" > "$OBJ/build_id.cpp"
 /opt/rocm/bin/hipcc -O2 -fPIC -c -o "$OBJ/build_id.o" "$OBJ/build_id.cpp"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$R/$OUT" "$OBJ"/*.o "$OBJ/build_id.o" -ldl
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$R/$OUT" "$OBJ"/*.o -ldl
 echo "built $OUT"
