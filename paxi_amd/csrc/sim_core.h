@@ -1105,6 +1105,49 @@ __device__ __forceinline__ void wb_flush(Rep<NT>& x) {
     x.ci = ~0u;
   }
 }
+// Replica order per lane (PXS_BUSY_FIRST).  The replica-steps of one step are
+// independent - every send lands in a later step's bucket - so each lane may
+// run its cluster's replicas in any order.  A wave's replica-step lasts as long
+// as its busiest lane's; with every lane taking its replicas busiest first
+// (inbox records, ties to the lower index), the k-th replica-step of the wave
+// meets the k-th busiest replica of every cluster, and a WPaxos wave no longer
+// waits at each of its nine replica-steps for whichever lane holds that
+// replica's leader burst (tools/imbalance.py: config 5 cost 3.24 -> 1.84x the
+// mean lane).  Returns the order as nibbles, first replica lowest.
+#ifndef PXS_BUSY_FIRST
+#define PXS_BUSY_FIRST 1
+#endif
+#ifndef PXS_BUSY_FIRST_ALL
+#define PXS_BUSY_FIRST_ALL 0   // 1: every protocol (A/B); default: the per-key protocol's kernels
+#endif
+template <int NT, class Proto> constexpr bool busy_first() {
+  return PXS_BUSY_FIRST && (PXS_BUSY_FIRST_ALL || Proto::kind == PAXISIM_WPAXOS);
+}
+template <int NT>
+__device__ __forceinline__ uint64_t replica_order(const Params& P, const Rep<NT>& x, uint32_t b0) {
+  constexpr uint32_t NMAX = NT ? (uint32_t)NT : (uint32_t)PAXISIM_MAX_N;
+  const uint32_t N = nrep<NT>(P), NS = N + 1u;
+  uint32_t key[NMAX];
+#pragma unroll
+  for (uint32_t r = 0; r < NMAX; r++) {
+    uint32_t n = 0;
+    if (r < N) {
+      const uint32_t box0 = (b0 * N + r) * NS;
+      for (uint32_t s = 0; s < NS; s++) n += x.l_cnt[((box0 + s) << 6) | x.lane];
+    }
+    key[r] = r < N ? (n << 4) | (15u - r) : 0u;   // distinct; more records first, then the lower index
+  }
+  uint64_t order = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < NMAX; r++) {
+    uint32_t rank = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < NMAX; q++) rank += key[q] > key[r] ? 1u : 0u;
+    if (r < N) order |= (uint64_t)r << (4u * rank);
+  }
+  return order;
+}
+
 #ifndef PXS_SERIAL_WAVES
 #define PXS_SERIAL_WAVES 2   // waves per SIMD the register budget must allow (2: <= 256 VGPRs; A/B r3: 3 waves at 168 VGPRs spill 127 and run 10-24% slower)
 #endif
@@ -1188,8 +1231,10 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
   uint32_t b0 = t0 % P.D;
   for (uint32_t t = t0; t < t0 + nsteps; t++) {
     if (live && x.l_poison[x.lane] >= t) {
+      const uint64_t order = busy_first<NT, Proto>() ? replica_order<NT>(P, x, b0) : 0x0FEDCBA987654321ull;
 #pragma nounroll
-      for (uint32_t r = 0; r < N; r++) {
+      for (uint32_t k = 0; k < N; k++) {
+        const uint32_t r = busy_first<NT, Proto>() ? (uint32_t)(order >> (4u * k)) & 15u : k;
         x.r = r;
         x.t = t;
         x.b0 = b0;

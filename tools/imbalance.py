@@ -14,6 +14,9 @@ largest lane count, against the mean (sum / 64):
   phase k      - sorted by the convoy phase: the step (mod k) at which the
                  cluster's leader was busiest in the previous half-window
   phase k (same window) - the same, measured on the priced window itself (a bound)
+  busiest_first - no re-binning; every lane runs its replicas busiest first
+                 (the serial kernel's PXS_BUSY_FIRST order)
+  lane_total_bound - lanes that advance through their replicas independently
 The oracle is the checker here, not the thing measured.
 usage: python tools/imbalance.py <config> <clusters> <start> <steps> [out.json]"""
 import argparse
@@ -79,6 +82,13 @@ def main():
             for t in range(lo, hi):
                 ph[:, (start + t) % k] += lead[t]
             res[name] = cost(np.lexsort((ph.sum(axis=1), np.argmax(ph, axis=1))), h, T)
+    # replica order per lane: each lane runs its replicas busiest first (the
+    # step's counts are known before any replica runs), so the k-th replica-step
+    # of every lane in a wave is its k-th busiest; and the bound where lanes
+    # advance through their replicas independently (no shared replica index)
+    Xp = Ml[h:T].reshape(T - h, L // 64, 64, -1)
+    res["busiest_first"] = float((-np.sort(-Xp, axis=3)).max(axis=2).sum() / (Ml[h:T].sum() / 64.0))
+    res["lane_total_bound"] = float(Xp.sum(axis=3).max(axis=2).sum() / (Ml[h:T].sum() / 64.0))
     x = lead.astype(float) - lead.mean(axis=0)
     res["leader_autocorrelation"] = {str(g): float((x[g:] * x[:-g]).sum() / (x * x).sum()) for g in range(1, 7)}
     out = json.dumps(res, indent=1)

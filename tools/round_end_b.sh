@@ -13,10 +13,12 @@ head -c 400 "$OUT/bench_config2.json"; echo
 export TMPDIR=/tmp
 ( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python "$R/bench.py" --no-cpu-baseline --no-shard-check > "$OUT/prof.log" 2>&1 ) || { echo "rocprof failed"; tail -5 "$OUT/prof.log"; exit 1; }
 python3 tools/prof_timed.py "$(find "$OUT/prof" -name '*kernel_trace.csv' | head -n1)" 0 "$OUT/bench_config2.json" > "$OUT/prof_timed.json" && cat "$OUT/prof_timed.json"
-for c in 3 4 5; do
+for c in 1 3 4 5; do
   timeout -k 10 500 python bench.py --config $c > "$OUT/bench_config$c.json" 2> "$OUT/bench_config$c.err" || { echo "config $c failed"; tail -5 "$OUT/bench_config$c.err"; exit 1; }
   head -c 300 "$OUT/bench_config$c.json"; echo
 done
+timeout -k 10 500 python bench.py --config 4 --fz 0 > "$OUT/bench_config4_fz0.json" 2> "$OUT/bench_config4_fz0.err" || { echo "config 4 fz0 failed"; tail -5 "$OUT/bench_config4_fz0.err"; exit 1; }
+head -c 300 "$OUT/bench_config4_fz0.json"; echo
 timeout -k 10 300 python tools/stamps.py 262144 2000 300 2 > "$OUT/stamps_config2.txt" 2>&1
 timeout -k 10 300 python tools/stamps.py 65536 1000 300 5 > "$OUT/stamps_config5.txt" 2>&1
 timeout -k 10 300 python tools/stamps.py 65536 1000 300 4 > "$OUT/stamps_config4.txt" 2>&1
