@@ -1113,15 +1113,16 @@ __device__ __forceinline__ void wb_flush(Rep<NT>& x) {
 // meets the k-th busiest replica of every cluster, and a WPaxos wave no longer
 // waits at each of its nine replica-steps for whichever lane holds that
 // replica's leader burst (tools/imbalance.py: config 5 cost 3.24 -> 1.84x the
-// mean lane).  Returns the order as nibbles, first replica lowest.
+// mean lane; A/B r4h/r4i: config 5 +32%, config 3 +8%).  Returns the order as
+// nibbles, first replica lowest.
 #ifndef PXS_BUSY_FIRST
 #define PXS_BUSY_FIRST 1
 #endif
 #ifndef PXS_BUSY_FIRST_ALL
-#define PXS_BUSY_FIRST_ALL 0   // 1: every protocol (A/B); default: the per-key protocol's kernels
+#define PXS_BUSY_FIRST_ALL 0   // 1: every protocol (A/B r4i: Paxos -2% on config 2, -4% on config 4); default: WPaxos and ABD
 #endif
 template <int NT, class Proto> constexpr bool busy_first() {
-  return PXS_BUSY_FIRST && (PXS_BUSY_FIRST_ALL || Proto::kind == PAXISIM_WPAXOS);
+  return PXS_BUSY_FIRST && (PXS_BUSY_FIRST_ALL || Proto::kind == PAXISIM_WPAXOS || Proto::kind == PAXISIM_ABD);
 }
 template <int NT>
 __device__ __forceinline__ uint64_t replica_order(const Params& P, const Rep<NT>& x, uint32_t b0) {
