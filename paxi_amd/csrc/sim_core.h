@@ -1149,6 +1149,9 @@ __device__ __forceinline__ uint64_t replica_order(const Params& P, const Rep<NT>
   return order;
 }
 
+#ifndef PXS_PHASE_HYST
+#define PXS_PHASE_HYST 0   // percent a new residue must lead the current one by (phase binning)
+#endif
 #ifndef PXS_SERIAL_WAVES
 #define PXS_SERIAL_WAVES 2   // waves per SIMD the register budget must allow (2: <= 256 VGPRs; A/B r3: 3 waves at 168 VGPRs spill 127 and run 10-24% slower)
 #endif
@@ -1290,6 +1293,12 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
         const uint32_t v = ph[(k << 6) | x.lane];
         if (v > most) { most = v; best = k; }
       }
+      // hysteresis: a cluster keeps its residue unless the new one leads it by
+      // more than PXS_PHASE_HYST percent, so near-ties do not move it back and forth
+      const uint32_t prev = P.phase[x.c];
+      if (PXS_PHASE_HYST && prev < P.phase_period && prev != best &&
+          most * 100u <= ph[(prev << 6) | x.lane] * (100u + PXS_PHASE_HYST))
+        best = prev;
       P.phase[x.c] = best;
     }
   }

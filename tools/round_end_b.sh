@@ -13,7 +13,9 @@ head -c 400 "$OUT/bench_config2.json"; echo
 export TMPDIR=/tmp
 ( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python "$R/bench.py" --no-cpu-baseline --no-shard-check > "$OUT/prof.log" 2>&1 ) || { echo "rocprof failed"; tail -5 "$OUT/prof.log"; exit 1; }
 python3 tools/prof_timed.py "$(find "$OUT/prof" -name '*kernel_trace.csv' | head -n1)" 0 "$OUT/bench_config2.json" > "$OUT/prof_timed.json" && cat "$OUT/prof_timed.json"
-for c in 1 3 4 5; do
+timeout -k 10 300 python bench.py --config 1 --warmup 0 --steps 1 > "$OUT/bench_config1.json" 2> "$OUT/bench_config1.err" || { echo "config 1 failed"; tail -5 "$OUT/bench_config1.err"; exit 1; }
+head -c 300 "$OUT/bench_config1.json"; echo
+for c in 3 4 5; do
   timeout -k 10 500 python bench.py --config $c > "$OUT/bench_config$c.json" 2> "$OUT/bench_config$c.err" || { echo "config $c failed"; tail -5 "$OUT/bench_config$c.err"; exit 1; }
   head -c 300 "$OUT/bench_config$c.json"; echo
 done
