@@ -1149,6 +1149,9 @@ __device__ __forceinline__ uint64_t replica_order(const Params& P, const Rep<NT>
   return order;
 }
 
+#ifndef PXS_PHASE_RECENT
+#define PXS_PHASE_RECENT 0   // 1: the residue counts cover the launch's second half only (fresher phase)
+#endif
 #ifndef PXS_PHASE_HYST
 #define PXS_PHASE_HYST 0   // percent a new residue must lead the current one by (phase binning)
 #endif
@@ -1234,6 +1237,8 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
   x.kc = live ? P.kc[x.c] : 0u;
   uint32_t b0 = t0 % P.D;
   for (uint32_t t = t0; t < t0 + nsteps; t++) {
+    if (PXS_PHASE_RECENT && P.phase_sort && t == t0 + nsteps / 2u)   // the launch's second half only
+      for (uint32_t k = 0; k < P.phase_period; k++) reinterpret_cast<uint32_t*>(x.l_cnt + P.ph_rel)[(k << 6) | x.lane] = 0;
     if (live && x.l_poison[x.lane] >= t) {
       const uint64_t order = busy_first<NT, Proto>() ? replica_order<NT>(P, x, b0) : 0x0FEDCBA987654321ull;
 #pragma nounroll
