@@ -257,6 +257,7 @@ struct oracle_sim {
   uint32_t variant;                /* per-key protocol (cfg.protocol reads WPAXOS): WPAXOS, M2PAXOS, KPAXOS */
   uint32_t zfirst[PAXISIM_MAX_ZONES]; /* replica index of "z.1" */
   uint32_t AR;                     /* agreement ring: checkpoints kept per (cluster, instance) */
+  uint32_t order;                  /* test hook: replica order within a step (oracle_set_replica_order) */
   int kv;                          /* replicas keep the Database (paxisim_config.kv) */
   uint32_t* move_cdf;              /* moving-Mu key CDF tables (a copy of paxisim_workload.move_cdf) */
 };
@@ -1606,9 +1607,32 @@ static void replica_step(const struct oracle_sim* s, cluster_t* c, uint32_t r, u
 }
 
 static void cluster_step(const struct oracle_sim* s, cluster_t* c, uint32_t t) {
-  uint32_t r;
+  uint32_t r, k, perm[PAXISIM_MAX_N];
   if (c->poison_step < t) return;                          /* a panic froze the process */
-  for (r = 0; r < s->N; r++) replica_step(s, c, r, t);
+  if (!s->order) {
+    for (r = 0; r < s->N; r++) replica_step(s, c, r, t);
+    return;
+  }
+  /* test hook: the replicas of the step in another order - reversed (1), or
+   * shuffled per (cluster, step) by a hash (2) - to check that a step's
+   * replica-steps are independent (DESIGN.md §3.3, §5.6 busiest first) */
+  for (r = 0; r < s->N; r++) perm[r] = s->order == 1 ? s->N - 1u - r : r;
+  if (s->order == 2) {
+    uint32_t h = (uint32_t)(c - s->cl) * 0x9E3779B1u ^ t * 0x85EBCA77u;
+    for (k = s->N - 1u; k > 0; k--) {
+      uint32_t j, tmp;
+      h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12;
+      j = h % (k + 1u);
+      tmp = perm[k]; perm[k] = perm[j]; perm[j] = tmp;
+    }
+  }
+  for (k = 0; k < s->N; k++) replica_step(s, c, perm[k], t);
+}
+
+int oracle_set_replica_order(oracle_sim* s, uint32_t mode) {
+  if (!s || mode > 2) return fail(PAXISIM_EINVAL, "replica order mode");
+  s->order = mode;
+  return 0;
 }
 
 /* ------------------------------------------------------------------------ */

@@ -27,6 +27,8 @@ int  oracle_destroy(oracle_sim* h);
 int  oracle_fault_add(oracle_sim* h, const paxisim_fault* f);
 /* nthreads > 1 shards clusters over POSIX threads (CPU baseline only). */
 int  oracle_step(oracle_sim* h, uint32_t nsteps, int nthreads);
+/* test hook: 0 runs a step's replicas in index order, 1 reversed, 2 shuffled per (cluster, step) */
+int  oracle_set_replica_order(oracle_sim* h, uint32_t mode);
 int  oracle_stats_get(oracle_sim* h, paxisim_stats* out);
 int  oracle_read_state(oracle_sim* h, uint64_t cluster_lo, uint64_t n,
                        paxisim_replica_state* out);

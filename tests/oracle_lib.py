@@ -63,6 +63,10 @@ class OracleSim:
     def step(self, n, threads=1):
         _check(lib().oracle_step(self.h, n, threads))
 
+    def set_replica_order(self, mode):
+        """Test hook: 0 = index order, 1 = reversed, 2 = shuffled per (cluster, step)."""
+        _check(lib().oracle_set_replica_order(self.h, mode))
+
     def stats(self):
         s = abi.Stats()
         _check(lib().oracle_stats_get(self.h, C.byref(s)))
