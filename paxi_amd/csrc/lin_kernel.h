@@ -54,6 +54,9 @@ __device__ __forceinline__ uint32_t lin_now() {
 enum { LS_P1 = 0, LS_P2, LS_SORT, LS_RUN, LS_ADD, LS_LOOK, LS_MERGE, LS_REACH };
 
 constexpr uint32_t LIN_LW = 4;             // waves per cluster workgroup
+#ifndef PXS_LIN_MINW
+#define PXS_LIN_MINW 8   // waves per SIMD the cluster kernel's registers must allow (A/B r4t: scan 0.99 -> 0.96 s at 64 VGPRs, 9 spilled)
+#endif
 constexpr uint32_t LIN_SMAX = 128;         // partitions checked in LDS by the cluster kernel
 constexpr uint32_t LIN_WPL_MAX = 4;        // bit-set words per lane: up to 4096 * 4 vertices
 constexpr uint32_t LIN_VMAX = 4096u * LIN_WPL_MAX;   // larger partitions are counted as skipped
@@ -708,7 +711,7 @@ __device__ __forceinline__ const uint4* hist_at(const Params& P, uint64_t c, con
 // [grid][N*H] ops, the cluster's history grouped by key (its own region of
 // the launch's workspace).  Dynamic LDS: LIN_LW sort buffers (LIN_SORT_BYTES);
 // partitions of at most LIN_SMAX ops are checked in registers (LinReg).
-__global__ void __launch_bounds__(LIN_LW * 64) lin_cluster_kernel(Params P, uint64_t c0, uint4* stage_all,
+__global__ void __launch_bounds__(LIN_LW * 64, PXS_LIN_MINW) lin_cluster_kernel(Params P, uint64_t c0, uint4* stage_all,
                                                                    unsigned long long* out, uint2* big) {
   extern __shared__ uint4 lds_lin[];
   __shared__ uint32_t len[PAXISIM_MAX_N];
