@@ -53,7 +53,10 @@ __device__ __forceinline__ uint32_t lin_now() {
 #endif
 enum { LS_P1 = 0, LS_P2, LS_SORT, LS_RUN, LS_ADD, LS_LOOK, LS_MERGE, LS_REACH };
 
-constexpr uint32_t LIN_LW = 4;             // waves per cluster workgroup
+#ifndef PXS_LIN_LW
+#define PXS_LIN_LW 2   // (A/B r4w, config 3 scan: 2 waves 0.926 s, 4 waves 0.962 s, 8 waves 1.079 s)
+#endif
+constexpr uint32_t LIN_LW = PXS_LIN_LW;    // waves per cluster workgroup
 #ifndef PXS_LIN_MINW
 #define PXS_LIN_MINW 8   // waves per SIMD the cluster kernel's registers must allow (A/B r4t: scan 0.99 -> 0.96 s at 64 VGPRs, 9 spilled)
 #endif
