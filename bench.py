@@ -46,7 +46,15 @@ DEFAULTS = {1: dict(clusters=1, sim_steps=3010, window=32, mbox=16),
             3: dict(clusters=1 << 20, sim_steps=80, window=16, mbox=16),
             4: dict(clusters=1 << 19, sim_steps=200, window=16, mbox=24),
             5: dict(clusters=1 << 18, sim_steps=200, window=16, mbox=24)}
-LAUNCH_STEPS = int(os.environ.get("PAXISIM_LAUNCH_STEPS", "50"))   # virtual steps fused per kernel launch
+# virtual steps fused per kernel launch: 50, and config 3's whole 80-step bench
+# step in one launch (A/B r4ls2: 44.6 -> 45.8 G msgs/s; configs 2 and 5 are
+# best at 50); PAXISIM_LAUNCH_STEPS overrides
+LAUNCH_DEFAULT = {3: 80}
+
+
+def launch_steps(cfg_id):
+    env = os.environ.get("PAXISIM_LAUNCH_STEPS")
+    return int(env) if env else LAUNCH_DEFAULT.get(cfg_id, 50)
 
 
 def alg_bytes(delta):
@@ -80,7 +88,7 @@ def workload(cfg_id, clusters, base, device, args):
         # the reference's own CPU case (bin/simulation.sh): 3 replicas, one
         # client, 1000 sequential writes to 1.1, no faults; 3 steps a request
         cfg = abi.make_config(npz=[3], clusters=clusters, cluster_base=base, seed=1, window=args.window,
-                              mbox_cap=args.mbox, max_delay=0, steps_per_launch=LAUNCH_STEPS, device=device,
+                              mbox_cap=args.mbox, max_delay=0, steps_per_launch=launch_steps(cfg_id), device=device,
                               kv=args.kv)
         wl = abi.make_workload(outstanding=1, max_requests=1000, target=[0])
         return cfg, wl, None, [], {
@@ -88,7 +96,7 @@ def workload(cfg_id, clusters, base, device, args):
                         "(the reference's CPU case; run with --warmup 0 --steps 1)", "replicas": 3, "outstanding": 1}
     if cfg_id == 2:
         cfg = abi.make_config(npz=[5], clusters=clusters, cluster_base=base, seed=42, window=args.window,
-                              mbox_cap=args.mbox, max_delay=4, steps_per_launch=LAUNCH_STEPS, device=device,
+                              mbox_cap=args.mbox, max_delay=4, steps_per_launch=launch_steps(cfg_id), device=device,
                               kv=args.kv)
         wl = abi.make_workload(outstanding=8, target=0)
         fp = abi.make_fault_process(drop_ppm=1000, drop_len=50, slow_ppm=1000, slow_len=50, slow_min=1, slow_max=4)
@@ -98,7 +106,7 @@ def workload(cfg_id, clusters, base, device, args):
             "slow": "p=1e-3/step/link, 1-4 steps, 50-step windows"}
     if cfg_id == 3:
         cfg = abi.make_config(protocol=abi.ABD, npz=[5], clusters=clusters, cluster_base=base, seed=42, keys=16,
-                              mbox_cap=args.mbox, max_delay=4, steps_per_launch=LAUNCH_STEPS, device=device,
+                              mbox_cap=args.mbox, max_delay=4, steps_per_launch=launch_steps(cfg_id), device=device,
                               history=args.history)
         wl = abi.make_workload(outstanding=4, target=[0, 1, 2, 3], write_ppm=500_000)
         return cfg, wl, None, [], {
@@ -117,7 +125,7 @@ def workload(cfg_id, clusters, base, device, args):
         q1, q2 = (abi.Q_FGRID_Q1, abi.Q_FGRID_Q2) if fz else (abi.Q_GRID_ROW, abi.Q_GRID_COLUMN)
         cfg = abi.make_config(npz=[3, 3, 3], clusters=clusters, cluster_base=base, seed=42, q1=q1,
                               q2=q2, fz=fz, ephemeral_leader=1, window=args.window, mbox_cap=args.mbox,
-                              max_delay=0, steps_per_launch=LAUNCH_STEPS, device=device,
+                              max_delay=0, steps_per_launch=launch_steps(cfg_id), device=device,
                               kv=args.kv)
         wl = abi.make_workload(outstanding=8, target=[0, 0, 0, 0, 3, 3, 3, 3], start_step=[0, 0, 0, 0, c, c, c, c])
         faults = [abi.make_fault(abi.FAULT_CRASH, 0, step_from=c)]
@@ -131,7 +139,7 @@ def workload(cfg_id, clusters, base, device, args):
     if cfg_id == 5:
         cfg = abi.make_config(protocol=abi.WPAXOS, npz=[3, 3, 3], keys=8, fz=0, adaptive=1, policy_threshold=3,
                               clusters=clusters, cluster_base=base, seed=42, window=args.window, mbox_cap=args.mbox,
-                              max_delay=0, steps_per_launch=LAUNCH_STEPS, device=device,
+                              max_delay=0, steps_per_launch=launch_steps(cfg_id), device=device,
                               kv=args.kv)
         wl = abi.make_workload(outstanding=9, target=list(range(9)), locality_ppm=700_000)
         return cfg, wl, None, [], {
