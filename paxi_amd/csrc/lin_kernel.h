@@ -455,6 +455,10 @@ struct LinReg {
   uint32_t vid0, vid1;       // sorted op -> vertex, or LIN_NOV
   B2 row0, row1;             // successor rows of vertex j*64+lane
   uint32_t vst0, vst1, ven0, ven1, vvl0, vvl1, opv0, opv1;
+  // a lower bound of the (refined) ends of the vertex's successors: an edge
+  // u -> t with u.start > t.end - the only kind cut() removes - can exist only
+  // where vst > msc (run(): the cyclic-state shortcut)
+  uint32_t msc0, msc1;
   uint32_t stk0, stk1;       // DFS stack entry sp at lane sp & 63, slot sp >> 6
   // wave-uniform
   B2 present, writes;
@@ -501,6 +505,7 @@ struct LinReg {
     row0 = b2(0, 0);
     row1 = b2(0, 0);
     vst0 = vst1 = ven0 = ven1 = vvl0 = vvl1 = opv0 = opv1 = 0;
+    msc0 = msc1 = ~0u;
     stk0 = stk1 = 0;
   }
   // checker.add (checker.go:21-33)
@@ -517,9 +522,10 @@ struct LinReg {
     vst1 = n1 ? oz : vst1; ven1 = n1 ? ow : ven1; vvl1 = n1 ? oy : vvl1; opv1 = n1 ? o : opv1;
     row0.lo = n0 ? 0ull : row0.lo; row0.hi = n0 ? 0ull : row0.hi;
     row1.lo = n1 ? 0ull : row1.lo; row1.hi = n1 ? 0ull : row1.hi;
+    msc0 = n0 ? ~0u : msc0; msc1 = n1 ? ~0u : msc1;
     // v -> id for every present vertex that ended before o started (id is not yet present)
-    if (l < id && present.has(l) && ven0 < oz) row0.set(id);
-    if (l + 64u < id && present.has(l + 64u) && ven1 < oz) row1.set(id);
+    if (l < id && present.has(l) && ven0 < oz) { row0.set(id); msc0 = min(msc0, ow); }
+    if (l + 64u < id && present.has(l + 64u) && ven1 < oz) { row1.set(id); msc1 = min(msc1, ow); }
     present.set(id);
     if (ox >> 31) writes.set(id);
   }
@@ -545,9 +551,12 @@ struct LinReg {
   // merge (checker.go:55-67)
   __device__ __forceinline__ void merge(uint32_t r, uint32_t m) {
     const uint32_t l = lane_id();
+    const uint32_t er = ven_of(r), em = ven_of(m), emin = er < em ? er : em;
+    // the edges into m (old, and the read's inherited ones) now end at emin
+    if (l < nv && l != m && (row0.has(r) || row0.has(m))) msc0 = min(msc0, emin);
+    if (l + 64u < nv && l + 64u != m && (row1.has(r) || row1.has(m))) msc1 = min(msc1, emin);
     if (l < nv && l != m && row0.has(r)) row0.set(m);
     if (l + 64u < nv && l + 64u != m && row1.has(r)) row1.set(m);
-    const uint32_t er = ven_of(r), em = ven_of(m);
     if (er < em) {                                        // refine the merged vertex's response time
       const uint32_t om = rl(pick(m, opv0, opv1), m & 63u);
       ven0 = l == (m & 63u) && !(m >> 6) ? er : ven0;
@@ -601,7 +610,8 @@ struct LinReg {
           }
           if (u == ~0u) {
             uint64_t c = row_of(v, 1) & ~black.hi;
-            if (k > 64u) c &= ~0ull << (k - 64u);
+            if (k >= 128u) c = 0;                       // resumed after vertex 127: no successor left
+            else if (k > 64u) c &= ~0ull << (k - 64u);
             if (c) u = 64u + (uint32_t)__builtin_ctzll(c);
           }
           if (u == ~0u) {                                // v done: black, back to its parent
@@ -627,18 +637,26 @@ struct LinReg {
     }
     return false;
   }
-  // checker.go:93-100: remove the edges u->t between gray vertices with u.start > t.end
-  __device__ __forceinline__ void cut(const B2& gray) {
+  // checker.go:93-100: remove the edges u->t between gray vertices with u.start > t.end;
+  // returns whether any edge was removed
+  __device__ __forceinline__ bool cut(const B2& gray) {
     const uint32_t l = lane_id();
     const bool g0 = gray.has(l), g1 = gray.has(l + 64u);
+    bool ch = false;
     for (uint32_t w = 0; w < 2; w++) {
       for (uint64_t g = gray.w(w); g; g &= g - 1u) {
         const uint32_t t = w * 64u + (uint32_t)__builtin_ctzll(g);
         const uint32_t et = ven_of(t);
-        if (g0 && vst0 > et) row0.clr(t);
-        if (g1 && vst1 > et) row1.clr(t);
+        if (g0 && vst0 > et && row0.has(t)) { row0.clr(t); ch = true; }
+        if (g1 && vst1 > et && row1.has(t)) { row1.clr(t); ch = true; }
       }
     }
+    return __ballot(ch) != 0;
+  }
+  // May the graph hold an edge u -> t with u.start > t.end (one cut() would remove)?
+  __device__ __forceinline__ bool inverted_any() const {
+    const uint32_t l = lane_id();
+    return __ballot((present.has(l) && vst0 > msc0) || (present.has(l + 64u) && vst1 > msc1)) != 0;
   }
   // checker.linearizable (checker.go:69-104) over the sorted ops
   __device__ __forceinline__ uint32_t run() {
@@ -662,13 +680,25 @@ struct LinReg {
       B2 gray = b2(0, 0);
       const bool was_cyclic = maybe_cyclic;
       LIN_T0(tr)
+      // Cyclic-state shortcut (round 5).  Between checks the graph loses only
+      // edges into the merged read, a sink, so a cycle found before is still
+      // there and Cycle() finds one: an anomaly.  cut() then removes nothing
+      // when no edge u -> t has u.start > t.end anywhere (msc), and the graph
+      // stays cyclic - no DFS needed.  (Config 3: every cyclic-state read;
+      // tools/lin_model.py: DFS steps 2.67 -> 0.08 per op, anomalies equal.)
+      if (maybe_cyclic && !inverted_any()) {
+        anomalies++;
+        LIN_T1(tr, LS_REACH)
+        continue;
+      }
       if (maybe_cyclic) cyc = cycle(gray);
       else if (m != LIN_NOV && reaches_self(m)) cyc = cycle(gray);
       LIN_T1(tr, LS_REACH)
       if (cyc) {
         anomalies++;
-        cut(gray);
-        if (!was_cyclic) {
+        if (!cut(gray)) {
+          maybe_cyclic = true;                            // the graph is the one just found cyclic
+        } else if (!was_cyclic) {
           maybe_cyclic = reaches_self(m);
         } else {
           B2 g2;

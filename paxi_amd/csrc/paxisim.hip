@@ -491,20 +491,42 @@ __device__ __forceinline__ void swap_lanes(T* base, size_t bstride, size_t rows,
 }
 
 // Swap every per-slot datum of the Paxos step kernel between slots p and q
-// (one wave per pair, lane j takes every 64th element).
+// (one wave per pair, lane j takes every 64th element).  Only live data moves
+// (round 5): pending / forward entries past their counts and the ghost table
+// of a replica that never raised GHOST are never read before they are written
+// (paxos_kernel.h), so a pair moves max(count_p, count_q) of them; the
+// agreement ring is indexed by cluster id, not slot (sim_core.h agree_drain),
+// and does not move at all.
+static_assert(PMAX + FMAX == LANES, "swap_slots: one lane per pending / forwards entry");
 __device__ void swap_slots(const Params& P, uint64_t p, uint64_t q, uint32_t j) {
   const size_t C = P.C, N = P.N;
+  // live extents, read before any row moves (uniform across the wave)
+  for (uint32_t r = 0; r < N; r++) {
+    const size_t ip = (size_t)r * C + p, iq = (size_t)r * C + q;
+    const uint32_t np0 = P.npend[ip], np1 = P.npend[iq];
+    const uint32_t nf0 = P.nfwd[ip], nf1 = P.nfwd[iq];
+    const bool gh = ((P.flags[ip] | P.flags[iq]) & PAXISIM_F_GHOST) != 0u;
+    const uint32_t np = np0 > np1 ? np0 : np1, nf = nf0 > nf1 ? nf0 : nf1;
+    // lane j < 32: pending entry j, 32 <= j < 64: forwards entry j - 32 (PMAX = FMAX = 32)
+    uint32_t* a = nullptr;
+    if (j < PMAX && j < np) a = P.pend + ((size_t)j * P.NI + r) * C;
+    else if (j >= PMAX && j - PMAX < nf) a = P.fwd + ((size_t)(j - PMAX) * N + r) * C;
+    uint32_t vp = 0, vq = 0;
+    uint4 gp = make_uint4(0u, 0u, 0u, 0u), gq = gp;
+    uint4* g = nullptr;
+    if (gh && j < GMAX) g = P.gst + ((size_t)j * P.NI + r) * C;
+    if (a) { vp = a[p]; vq = a[q]; }
+    if (g) { gp = g[p]; gq = g[q]; }
+    if (a) { a[p] = vq; a[q] = vp; }
+    if (g) { g[p] = gq; g[q] = gp; }
+  }
   swap_rows(P.ballot, 7 * N, C, p, q, j);        // ballot slot execute meta flags npend nfwd
   swap_rows(P.digest, N, C, p, q, j);
   swap_rows(P.kc, 1, C, p, q, j);
-  swap_rows(P.pend, (size_t)PMAX * P.NI, C, p, q, j);
-  swap_rows(P.fwd, (size_t)FMAX * N, C, p, q, j);
   swap_rows(P.link_drop, 2 * N * N, C, p, q, j);   // link_drop then link_slow
   swap_rows(P.ck_e, (size_t)CKR * P.NI, C, p, q, j);
   swap_rows(P.ck_d, (size_t)CKR * P.NI, C, p, q, j);
-  swap_rows(P.gst, (size_t)GMAX * P.NI, C, p, q, j);
   swap_rows(P.stats, (size_t)NSTAT * N, C, p, q, j);
-  swap_rows(P.agr, (size_t)P.AR * P.NK, C, p, q, j);
   swap_rows(P.kv_val, P.kv ? (size_t)P.keys * N : 0, C, p, q, j);
   swap_rows(P.kv_ver, P.kv ? N : 0, C, p, q, j);
   swap_rows(P.wrep, P.WK, C, p, q, j);
@@ -1079,6 +1101,14 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
         P.ph_rel = P.lds_tail + P.lds_bytes - P.img.off_cnt;
         P.lds_bytes += P.phase_period * LANES * 4u;
         P.phase_sort = 1;
+      }
+      // check_config bounds the image tail and the arrival counts; the phase
+      // counts come on top of them: refuse here, not at the first launch
+      if (P.lds_bytes > LDS_MAX) {
+        const uint32_t b = P.lds_bytes;
+        delete h;
+        return fail(PAXISIM_EUNSUPP, "serial LDS %u B (image tail, arrival and phase counts) exceeds LDS (%u B): "
+                    "reduce window/max_delay/replicas or set PAXISIM_PHASE_SORT=0", b, LDS_MAX);
       }
     }
   }

@@ -149,7 +149,8 @@ struct Params {
   uint32_t* wpend;       // [blk][K][N][64][PMAX]
   uint4* wpx;            // [blk][K][N][64][3] majority {hits u16 x 16 (2 x uint4), {sum, start step}} / ema {s lo, s hi, zone}
   uint32_t* stats;       // [NSTAT][N][C]
-  unsigned long long* agr;  // [AR][NK][C] first executor's digest per checkpoint: k << 40 | 40-bit digest fold
+  unsigned long long* agr;  // [AR][NK][C] first executor's digest per checkpoint: k << 40 | 40-bit digest fold;
+                            // the C index is the local cluster id (not the slot: compaction leaves it in place)
   uint32_t AR;           // checkpoints kept per (cluster, instance); 0 = no agreement ring
   uint4* agq;            // [2][AGMAX][N][C] a step's ring arrivals {entry lo, entry hi, key, 0}, by step parity
   uint32_t off_agn;      // LDS byte offset of the arrival counts [2][N][lane] u8 (per tile, outside the image)

@@ -501,6 +501,9 @@ __device__ __forceinline__ void fault_process(const Params& P, Rep<NT>& x, uint3
 #ifndef PXS_ABSORB_ABD
 #define PXS_ABSORB_ABD 0
 #endif
+#ifndef PXS_WP_ABSORB
+#define PXS_WP_ABSORB 0   // WPaxos same-key P2b absorption (wpaxos_kernel.h): 0 off, 1 the r4l experiment, 2 fixed
+#endif
 #ifndef PXS_FLUSH_LATE
 #define PXS_FLUSH_LATE 1
 #endif
@@ -774,7 +777,8 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
 #endif
     PXS_SUB_T0(pxs_ab0)
     if constexpr ((Proto::kind == PAXISIM_PAXOS && (PXS_ABSORB9 || NT != 9)) ||
-                  (Proto::kind == PAXISIM_ABD && PXS_ABSORB_ABD)) {
+                  (Proto::kind == PAXISIM_ABD && PXS_ABSORB_ABD) ||
+                  (Proto::kind == PAXISIM_WPAXOS && PXS_WP_ABSORB)) {
       // Next messages whose handling is short and send-free (a P2b that does
       // not complete a quorum: paxos.go:270-297) are handled in this same
       // trip, up to PXS_ABSORB_MAX of them.  Order, counters and state are exactly as
@@ -888,7 +892,8 @@ __device__ __forceinline__ void agree_drain(const Params& P, const Rep<NT>& x, u
       const uint4 e = P.agq[(((size_t)par * AGMAX + j) * N + r) * P.C + x.c];
       const unsigned long long want = (unsigned long long)e.x | ((unsigned long long)e.y << 32);
       const uint32_t k = e.y >> 8;
-      unsigned long long* a = &P.agr[((size_t)(k % P.AR) * P.NK + e.z) * P.C + x.c];
+      // indexed by the cluster, not its slot: compaction does not move the ring (paxisim.hip swap_slots)
+      unsigned long long* a = &P.agr[((size_t)(k % P.AR) * P.NK + e.z) * P.C + (x.gid - P.cluster_base)];
       const unsigned long long v = *a;
       const uint32_t tv = (uint32_t)(v >> 40);
       if (v == 0ull || tv < k) {

@@ -239,6 +239,19 @@ __device__ __forceinline__ void wp_handle_request(const Params& P, Rep<NT>& x, u
   }
 }
 
+// Same-trip absorption of a P2b for the kpaxos still bound.
+//   0: off (default).
+//   1: the round-4 r4l experiment as DESIGN.md §5.6 describes it: the next
+//      P2b of the bound key runs p2b_absorb on the bound registers after the
+//      dispatch's unbind, and nothing writes them back again; nor is "bound"
+//      checked (load() leaves key 0 with another instance's registers).  A
+//      diagnostic build only: it loses HandleP2b's ballot adoption
+//      (paxos.go:281-284) whenever the absorbed P2b carries a higher ballot.
+//   2: the same absorption with an explicit bound key (none after load()) and
+//      the instance written back when the absorbed P2b changed ballot/active.
+// (the macro is defined in sim_core.h, whose merge loop calls absorb)
+constexpr uint32_t WP_UNBOUND = 0xFFFFu;   // x.key before the first bind of a replica-step (PXS_WP_ABSORB=2)
+
 // LDS: the instance scalars live in the tile's LDS image (wlds); else in HBM
 template <bool LDS>
 struct WPaxosProtoT {
@@ -252,8 +265,21 @@ struct WPaxosProtoT {
     x.e0 = 0;                        // entry of slot s: word 4*(s & (W-1)) of the lane's window
     x.es = 4;
     x.pstride = 1;
-    x.key = 0;
+    x.key = PXS_WP_ABSORB >= 2 ? WP_UNBOUND : 0u;
     x.ktag = 0;
+  }
+  // HandleP2b (paxos.go:270-310) of a next message in the same trip, without
+  // a bind: only a P2b of the kpaxos whose registers are bound, and only when
+  // it completes no quorum (p2b_absorb).  handleAccepted (replica.go:90-93)
+  // first dereferences r.paxi[m.Key]: a nil kpaxos goes to the full handler,
+  // which poisons.
+  template <int NT>
+  __device__ static __forceinline__ bool absorb(const Params& P, Rep<NT>& x, uint32_t src, const uint4& m) {
+    if (hdr_type(m.x) != PAXISIM_MSG_P2B || hdr_key(m.x) != x.key || !x.exists) return false;
+    const uint32_t b0 = x.ballot, a0 = x.active;
+    if (!p2b_absorb<NT>(P, x, src, m)) return false;
+    if (PXS_WP_ABSORB >= 2 && (x.ballot != b0 || x.active != a0)) wp_unbind<NT, LDS>(P, x);
+    return true;
   }
   template <int NT>
   __device__ static __forceinline__ void store(const Params& P, const Rep<NT>& x) {

@@ -150,10 +150,18 @@ class Codec:
     def __init__(self, sim, cluster):
         self.sim, self.cluster, self.cfg = sim, cluster, sim.cfg
         self.top = Topology(sim.cfg)
-        self.kval = lambda k: _wl.key_value(sim.wl, sim.cfg.keys, k)     # key index <-> Command.Key
+        self.kval = self._key_value                                       # key index <-> Command.Key
         self.kidx = lambda v: _wl.key_index(sim.wl, sim.cfg.keys, v)
         self.proto = sim.cfg.protocol
         self._cmd = {}
+
+    def _key_value(self, k):
+        # an exponential tail draw (index == keys) names a key the simulator
+        # has no state for; the replicas raised UNFAITHFUL
+        if k >= self.cfg.keys:
+            raise TraceError(f"key index {k} lies beyond the key space (an exponential tail draw): "
+                             "the simulator flags such commands UNFAITHFUL and cannot export them")
+        return _wl.key_value(self.sim.wl, self.cfg.keys, k)
 
     def _commands(self, cids):
         todo = sorted({c for c in cids if c and c not in self._cmd})

@@ -167,6 +167,9 @@ def set_distribution(w, name, keys=None, key_space=0, move_every=0, **kw):
     w._move_buf = None
     for i in range(abi.MAX_KEYS):
         w.key_cdf[i] = 0
+    if name == "conflict" and getattr(w, "key_min", 0) and keys and (key_space or keys) >= keys:
+        # the native check_keys refuses it too: Go's literal key 0 needs an index of its own
+        raise ValueError("conflict with key_min != 0 needs key_space < keys (literal key 0 has its own index)")
     if w.distribution != abi.DIST_TABLE:
         if move_every:
             raise ValueError("Move applies to the normal distribution")
@@ -211,6 +214,8 @@ def expected_pmf(w, keys, table=None):
         return [(edges[k + 1] - edges[k]) / 4294967296.0 for k in range(keys)]
     ks = w.key_space or keys
     if w.distribution == abi.DIST_CONFLICT:
+        if w.key_min and ks >= keys:
+            raise ValueError("conflict with key_min != 0 needs key_space < keys (literal key 0 has its own index)")
         c = w.conflicts / 100.0
         p = [(1 - c) / ks if k < ks else 0.0 for k in range(keys)]
         p[ks if w.key_min else 0] += c
@@ -222,6 +227,8 @@ def key_value(w, keys, k):
     """The key value the reference's Database sees for key index k (Command.Key)."""
     if k >= keys:
         raise ValueError(f"key index {k} lies beyond the key space (an exponential tail draw)")
+    if w.distribution == abi.DIST_CONFLICT and w.key_min and (w.key_space or keys) >= keys:
+        raise ValueError("conflict with key_min != 0 needs key_space < keys (literal key 0 has its own index)")
     if w.distribution == abi.DIST_TABLE:
         return k
     if w.distribution == abi.DIST_CONFLICT and w.key_min and k == (w.key_space or keys):

@@ -41,6 +41,27 @@ def gen_partition(rng, n):
     return ops
 
 
+def gen_future_reads(rng, n):
+    """n ops of one key where a read may return any write's value, one that
+    starts only after the read ended too: merges then refine a write's end
+    below its start, which makes edges u -> t with u.start > t.end that
+    cut() removes (checker.go:93-100), and exercises the checker's
+    cyclic-state shortcut and its fallback (lin_kernel.h LinReg::run)."""
+    kinds, t = [], 0
+    for _ in range(n):
+        t += rng.choice((0, 0, 1, 1, 2, 3))
+        kinds.append((t, t + rng.choice((0, 1, 2, 3, 5, 8)), rng.random() < 0.5))
+    nw = sum(1 for k in kinds if k[2])
+    ops, v = [], 1
+    for (start, end, w) in kinds:
+        if w:
+            ops.append((1, v, start, end))
+            v += 1
+        else:
+            ops.append((0, 0 if rng.random() < 0.05 or nw == 0 else rng.randint(1, nw), start, end))
+    return ops
+
+
 def load(sims, cluster, key, ops, N, H):
     """Spread one partition over the replicas' histories (canonical order: replica 0 first)."""
     per = -(-len(ops) // N)
@@ -52,7 +73,7 @@ def load(sims, cluster, key, ops, N, H):
     assert per <= H
 
 
-def run_case(seed, sizes, N=5, H=256):
+def run_case(seed, sizes, N=5, H=256, gen=gen_partition):
     rng = random.Random(seed)
     keys = len(sizes[0])
     cfg = abi.make_config(protocol=abi.ABD, npz=[N], clusters=len(sizes), keys=keys, history=H)
@@ -63,7 +84,7 @@ def run_case(seed, sizes, N=5, H=256):
     expect = 0
     for c, row in enumerate(sizes):
         for k, n in enumerate(row):
-            ops = gen_partition(rng, n)
+            ops = gen(rng, n)
             expect += ol.linearizable([(v if w else None, None if w else v, s, e) for (w, v, s, e) in ops])
             load((g, o), c, k, ops, N, H)
     for (c, r), ops in g.extra.items():
@@ -80,6 +101,19 @@ def run_case(seed, sizes, N=5, H=256):
 def test_small_partitions_match_oracle(seed):
     sizes = [[1 + (7 * c + 13 * k + seed) % 128 for k in range(6)] for c in range(12)]
     (ga, gn, gsk), (oa, on), expect = run_case(seed, sizes)
+    assert gsk == 0 and gn == on == sum(map(sum, sizes))
+    assert ga == oa == expect and expect > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [11, 12])
+def test_future_reads_match_oracle(seed):
+    """Reads of writes that start later: cut() removes edges, so the
+    cyclic-state shortcut must fall back to the DFS exactly where the
+    reference's Cycle() / cut would change the graph; register path (at most
+    128 ops) and big path."""
+    sizes = [[1 + (11 * c + 17 * k + seed) % 128 for k in range(6)] for c in range(10)] + [[129, 200, 64, 90, 128, 5]]
+    (ga, gn, gsk), (oa, on), expect = run_case(seed, sizes, gen=gen_future_reads)
     assert gsk == 0 and gn == on == sum(map(sum, sizes))
     assert ga == oa == expect and expect > 0
 

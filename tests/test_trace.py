@@ -375,3 +375,21 @@ def test_reply_value_travels_in_the_trace():
     back = trace.import_streams(a, 1, streams, sched)
     reps = [r for (t, s, d, recs) in back["msgs"] for r in recs if r[1] == trace.T_REPLY]
     assert any(r[2] for r in reps)
+
+
+def test_export_refuses_exponential_tail_commands():
+    """An exponential tail draw (key index == keys) has no Command.Key in the
+    model: the codec raises TraceError, not a bare ValueError
+    (ADVICE r4)."""
+    cfg = abi.make_config(npz=[3], clusters=2, seed=4, keys=4, kv=1)
+    wl = abi.make_workload(outstanding=2, target=0, write_ppm=500_000, distribution="exponential", keys=4, lam=0.1)
+    a = OracleSim(cfg, wl)
+    codec = trace.Codec(a, 0)
+    tail = [c for c in range(1, 400) if a.command(0, c)[0] == 4]
+    fine = [c for c in range(1, 400) if a.command(0, c)[0] < 4]
+    assert tail and fine
+    codec._commands([tail[0], fine[0]])
+    assert codec.command(fine[0])["Key"] == a.command(0, fine[0])[0]
+    with pytest.raises(trace.TraceError):
+        codec.command(tail[0])
+    a.close()

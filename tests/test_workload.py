@@ -198,3 +198,18 @@ def test_bad_key_workloads_are_rejected():
     w.move_loop = w.move_tables
     with pytest.raises(RuntimeError):
         ol.OracleSim(cfg, w)
+
+
+def test_conflict_with_min_needs_its_own_key_index():
+    """check_keys refuses conflict with key_min != 0 and key_space >= keys; the
+    Python helpers raise the same ValueError instead of an IndexError."""
+    with pytest.raises(ValueError):
+        abi.make_workload(distribution="conflict", conflicts=40, key_min=100, keys=8)
+    wl = abi.make_workload(distribution="conflict", conflicts=40, key_min=100)   # keys unknown here
+    with pytest.raises(ValueError):
+        W.expected_pmf(wl, 8)
+    with pytest.raises(ValueError):
+        W.key_value(wl, 8, 0)
+    ok = abi.make_workload(distribution="conflict", conflicts=40, key_min=100, key_space=7, keys=8)
+    p = W.expected_pmf(ok, 8)
+    assert abs(sum(p) - 1.0) < 1e-9 and abs(p[7] - 0.4) < 1e-9

@@ -1,6 +1,8 @@
 #!/bin/bash
 # Build a variant of libpaxisim.so with extra compile flags (A/B and diagnostics).
 # Usage: tools/build_variant.sh <out.so> [-DFLAG=V ...]     (run in this container, not on the GPU box)
+# BASEFLAGS replaces __graft_entry__.HIP_FLAGS (e.g. without -disable-machine-sink); the variant's build
+# id is the sources' fingerprint + a hash of BASEFLAGS and the extra flags.
 set -e -o pipefail
 OUT=$1; shift
 R=$(cd "$(dirname "$0")/.." && pwd)
@@ -16,7 +18,7 @@ for s in $SRCS; do
 done
 for p in "${pids[@]}"; do wait "$p"; done
 # the variant's own build id: the sources' fingerprint + its extra flags
-VID="$(python3 -c "import __graft_entry__ as g; print(g.source_id())")+$(echo "$@" | md5sum | cut -c1-8)"
+VID="$(python3 -c "import __graft_entry__ as g; print(g.source_id())")+$(echo "${BASEFLAGS:-} $@" | md5sum | cut -c1-8)"
 printf 'extern "C" const char* paxisim_build_id(void) { return "%s"; }\n' "$VID" > "$OBJ/build_id.cpp"
 /opt/rocm/bin/hipcc -O2 -fPIC -c -o "$OBJ/build_id.o" "$OBJ/build_id.cpp"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$R/$OUT" "$OBJ"/*.o -ldl
