@@ -501,6 +501,9 @@ __device__ __forceinline__ void fault_process(const Params& P, Rep<NT>& x, uint3
 #ifndef PXS_ABSORB_ABD
 #define PXS_ABSORB_ABD 0
 #endif
+#ifndef PXS_AGR_SLOT
+#define PXS_AGR_SLOT 0    // 1: the ring indexed by slot (round 4; diagnostic A/B only - wrong under compaction)
+#endif
 #ifndef PXS_WP_ABSORB
 #define PXS_WP_ABSORB 0   // WPaxos same-key P2b absorption (wpaxos_kernel.h): 0 off, 1 the r4l experiment, 2 fixed
 #endif
@@ -879,6 +882,13 @@ __device__ __forceinline__ void agree_post(const Params& P, Rep<NT>& x, uint32_t
   }
   if (n < 255u) *cp = (uint8_t)(n + 1u);
 }
+// ABD and EPaxos keep no agreement ring (P.AR = 0): their kernels carry no
+// drain code at all (round 5: a change inside the never-run drain moved the
+// ABD kernel's code and cost config 3 9% - the kernels are sensitive to code
+// placement)
+template <class Proto> constexpr bool has_ring() {
+  return Proto::kind != PAXISIM_ABD && Proto::kind != PAXISIM_EPAXOS;
+}
 template <int NT>
 __device__ __forceinline__ void agree_drain(const Params& P, const Rep<NT>& x, uint32_t par) {
   const uint32_t N = nrep<NT>(P);
@@ -893,7 +903,8 @@ __device__ __forceinline__ void agree_drain(const Params& P, const Rep<NT>& x, u
       const unsigned long long want = (unsigned long long)e.x | ((unsigned long long)e.y << 32);
       const uint32_t k = e.y >> 8;
       // indexed by the cluster, not its slot: compaction does not move the ring (paxisim.hip swap_slots)
-      unsigned long long* a = &P.agr[((size_t)(k % P.AR) * P.NK + e.z) * P.C + (x.gid - P.cluster_base)];
+      const uint64_t cl = PXS_AGR_SLOT ? x.c : x.gid - P.cluster_base;
+      unsigned long long* a = &P.agr[((size_t)(k % P.AR) * P.NK + e.z) * P.C + cl];
       const unsigned long long v = *a;
       const uint32_t tv = (uint32_t)(v >> 40);
       if (v == 0ull || tv < k) {
@@ -1028,7 +1039,8 @@ __global__ void __launch_bounds__(max_threads<NT>(), min_waves<NT>()) sim_steps(
     st.barrier += stamp() - sb;
     st.steps++;
 #endif
-    if (P.AR && live && x.r == N - 1u) agree_drain<NT>(P, x, t & 1u);   // this step's arrivals, replica order
+    if constexpr (has_ring<Proto>())
+      if (P.AR && live && x.r == N - 1u) agree_drain<NT>(P, x, t & 1u);   // this step's arrivals, replica order
   }
 #ifdef PXS_STAMPS
   if (x.lane == 0 && P.dbg) {
@@ -1288,7 +1300,8 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
         rep_counters_flush<NT>(P, x);
       }
     }
-    if (P.AR && live) agree_drain<NT>(P, x, t & 1u);   // this step's arrivals, replica order
+    if constexpr (has_ring<Proto>())
+      if (P.AR && live) agree_drain<NT>(P, x, t & 1u);   // this step's arrivals, replica order
     if (++b0 == P.D) b0 = 0;
   }
   if (P.compact && live) {

@@ -25,3 +25,5 @@ step ab_c5 900 tools/ab_env.sh r5a/ab_c5 "prod1|X=1" "abs2a|PAXISIM_LIB=var/libp
   "abs2b|PAXISIM_LIB=var/libpaxisim_wpabs2.so" -- --config 5
 step ab_c2 900 tools/ab_env.sh r5a/ab_c2 "prod1|X=1" "r4a|PAXISIM_LIB=var/libpaxisim_r4.so" "prod2|X=1" \
   "r4b|PAXISIM_LIB=var/libpaxisim_r4.so" -- --config 2
+step ab_c3 900 tools/ab_env.sh r5a/ab_c3 "prod1|X=1" "r4a|PAXISIM_LIB=var/libpaxisim_r4.so" "prod2|X=1" \
+  "r4b|PAXISIM_LIB=var/libpaxisim_r4.so" -- --config 3

@@ -55,5 +55,6 @@ def diverges(case):
 
 
 if __name__ == "__main__":
+    names = sys.argv[1:] or list(CASES)   # e.g. `wp_crash` alone for a pass bisection (tools/bisect_pass.sh)
     print(json.dumps({"lib": os.environ.get("PAXISIM_LIB", "paxi_amd/libpaxisim.so"), "build_id": build_id(),
-                      "diverged": {c: diverges(c) for c in CASES}}), flush=True)
+                      "diverged": {c: diverges(c) for c in names}}), flush=True)
