@@ -58,7 +58,11 @@ enum { LS_P1 = 0, LS_P2, LS_SORT, LS_RUN, LS_ADD, LS_LOOK, LS_MERGE, LS_REACH };
 #endif
 constexpr uint32_t LIN_LW = PXS_LIN_LW;    // waves per cluster workgroup
 #ifndef PXS_LIN_MINW
-#define PXS_LIN_MINW 8   // waves per SIMD the cluster kernel's registers must allow (A/B r4t: scan 0.99 -> 0.96 s at 64 VGPRs, 9 spilled)
+// waves per SIMD the cluster kernel's registers must allow.  A/B r4t: 8 waves
+// (64 VGPRs, 9 spilled) 0.99 -> 0.96 s; round 5 (the cyclic-state shortcut's
+// fields, gpurun_out/r5c/ab_lin): 8 waves spill 40 VGPRs and scan in 0.82 s,
+// 7 waves (72 VGPRs, 16 spilled) 0.49 s, 6 (80, 2) 0.50 s, 5 (84, 0) 0.52 s
+#define PXS_LIN_MINW 7
 #endif
 constexpr uint32_t LIN_SMAX = 128;         // partitions checked in LDS by the cluster kernel
 constexpr uint32_t LIN_WPL_MAX = 4;        // bit-set words per lane: up to 4096 * 4 vertices

@@ -1732,9 +1732,15 @@ extern "C" int paxisim_linearizable(paxisim* h, uint64_t* anomalies, uint64_t* o
   HIPCHK(hipSetDevice(h->cfg.device));
   HIPCHK(hipStreamSynchronize(h->stream));
   const Params& P = h->P;
-  // clusters per launch: each gets a stage of N*H ops (its history grouped by key)
+  // clusters per launch: each gets a stage of N*H ops (its history grouped by key).
+  // The stage takes up to a quarter of the free HBM (2-16 GiB): fewer, longer
+  // launches leave less of each launch's last round of workgroups idle
+  // (config 3: 21 -> 6 launches); PAXISIM_LIN_STAGE_MB overrides (A/B).
   const size_t cap = (size_t)P.N * P.H;
-  const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(P.clusters, (2ull << 30) / (cap * sizeof(uint4))));
+  size_t budget = 2ull << 30, freeb = 0, totb = 0;
+  if (hipMemGetInfo(&freeb, &totb) == hipSuccess) budget = std::max(budget, std::min<size_t>(freeb / 4, 16ull << 30));
+  if (const char* e = getenv("PAXISIM_LIN_STAGE_MB")) budget = std::max<size_t>(1, (size_t)atoll(e)) << 20;
+  const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(P.clusters, budget / (cap * sizeof(uint4))));
   uint4* stage = nullptr;
   uint2* big = nullptr;
   unsigned long long* out = nullptr;

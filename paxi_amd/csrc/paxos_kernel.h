@@ -182,9 +182,35 @@ __device__ __forceinline__ void node_forward(const Params& P, Rep<NT>& x, uint32
   post_unicast<NT>(P, x, to, PAXISIM_MSG_REQUEST, 0u, 0u, cid);
 }
 
-// node.recv Reply case (node.go:83-90)
+// node.recv Reply case (node.go:83-90).  With the table in HBM (the per-key
+// kernels) the probe keeps the four entries it loaded: the request found is
+// one of them, and so is the table's last entry (moved into the freed place)
+// whenever it lies in the same group - one round trip where the LDS-window
+// kernels' probe-then-reload path takes three.
 template <int NT>
 __device__ __forceinline__ void handle_reply(const Params& P, Rep<NT>& x, uint32_t cid, uint32_t value) {
+  if (hbm_log(x)) {
+    const uint32_t last = x.nfwd - 1u;
+    for (uint32_t i0 = 0; i0 < x.nfwd; i0 += 4u) {
+      uint32_t f[4];
+#pragma unroll
+      for (uint32_t k = 0; k < 4u; k++) f[k] = i0 + k < x.nfwd ? P.fwd[krc(P, i0 + k, x.r, x.c)] : 0u;
+#pragma unroll
+      for (uint32_t k = 0; k < 4u; k++) {
+        if (!(i0 + k < x.nfwd && req_cid(f[k]) == cid)) continue;
+        uint32_t lv = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4u; q++) lv = last == i0 + q ? f[q] : lv;
+        if (last >= i0 + 4u) lv = ldg(&P.fwd[krc(P, last, x.r, x.c)]);
+        x.nfwd = last;
+        P.fwd[krc(P, i0 + k, x.r, x.c)] = lv;
+        request_reply<NT>(P, x, f[k], cid, value);
+        return;
+      }
+    }
+    x.flags |= PAXISIM_F_UNFAITHFUL;
+    return;
+  }
   const uint32_t i = fwd_find<NT>(P, x, cid);
   if (i == x.nfwd) {
     x.flags |= PAXISIM_F_UNFAITHFUL;

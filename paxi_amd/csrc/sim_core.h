@@ -502,7 +502,7 @@ __device__ __forceinline__ void fault_process(const Params& P, Rep<NT>& x, uint3
 #define PXS_ABSORB_ABD 0
 #endif
 #ifndef PXS_AGR_SLOT
-#define PXS_AGR_SLOT 0    // 1: the ring indexed by slot (round 4; diagnostic A/B only - wrong under compaction)
+#define PXS_AGR_SLOT 0    // 1: the Multi-Paxos ring indexed by slot too (round 4; diagnostic A/B only - wrong under compaction)
 #endif
 #ifndef PXS_WP_ABSORB
 #define PXS_WP_ABSORB 0   // WPaxos same-key P2b absorption (wpaxos_kernel.h): 0 off, 1 the r4l experiment, 2 fixed
@@ -882,14 +882,7 @@ __device__ __forceinline__ void agree_post(const Params& P, Rep<NT>& x, uint32_t
   }
   if (n < 255u) *cp = (uint8_t)(n + 1u);
 }
-// ABD and EPaxos keep no agreement ring (P.AR = 0): their kernels carry no
-// drain code at all (round 5: a change inside the never-run drain moved the
-// ABD kernel's code and cost config 3 9% - the kernels are sensitive to code
-// placement)
-template <class Proto> constexpr bool has_ring() {
-  return Proto::kind != PAXISIM_ABD && Proto::kind != PAXISIM_EPAXOS;
-}
-template <int NT>
+template <int NT, class Proto>
 __device__ __forceinline__ void agree_drain(const Params& P, const Rep<NT>& x, uint32_t par) {
   const uint32_t N = nrep<NT>(P);
   for (uint32_t r = 0; r < N; r++) {
@@ -902,8 +895,10 @@ __device__ __forceinline__ void agree_drain(const Params& P, const Rep<NT>& x, u
       const uint4 e = P.agq[(((size_t)par * AGMAX + j) * N + r) * P.C + x.c];
       const unsigned long long want = (unsigned long long)e.x | ((unsigned long long)e.y << 32);
       const uint32_t k = e.y >> 8;
-      // indexed by the cluster, not its slot: compaction does not move the ring (paxisim.hip swap_slots)
-      const uint64_t cl = PXS_AGR_SLOT ? x.c : x.gid - P.cluster_base;
+      // indexed by the cluster, not its slot: compaction does not move the ring
+      // (paxisim.hip swap_slots).  Only Multi-Paxos compacts; elsewhere slot ==
+      // cluster, and x.c keeps those kernels' code as it was
+      const uint64_t cl = Proto::kind == PAXISIM_PAXOS && !PXS_AGR_SLOT ? x.gid - P.cluster_base : x.c;
       unsigned long long* a = &P.agr[((size_t)(k % P.AR) * P.NK + e.z) * P.C + cl];
       const unsigned long long v = *a;
       const uint32_t tv = (uint32_t)(v >> 40);
@@ -1039,8 +1034,7 @@ __global__ void __launch_bounds__(max_threads<NT>(), min_waves<NT>()) sim_steps(
     st.barrier += stamp() - sb;
     st.steps++;
 #endif
-    if constexpr (has_ring<Proto>())
-      if (P.AR && live && x.r == N - 1u) agree_drain<NT>(P, x, t & 1u);   // this step's arrivals, replica order
+    if (P.AR && live && x.r == N - 1u) agree_drain<NT, Proto>(P, x, t & 1u);   // this step's arrivals, replica order
   }
 #ifdef PXS_STAMPS
   if (x.lane == 0 && P.dbg) {
@@ -1300,8 +1294,7 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
         rep_counters_flush<NT>(P, x);
       }
     }
-    if constexpr (has_ring<Proto>())
-      if (P.AR && live) agree_drain<NT>(P, x, t & 1u);   // this step's arrivals, replica order
+    if (P.AR && live) agree_drain<NT, Proto>(P, x, t & 1u);   // this step's arrivals, replica order
     if (++b0 == P.D) b0 = 0;
   }
   if (P.compact && live) {

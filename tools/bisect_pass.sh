@@ -3,7 +3,7 @@
 # per -opt-bisect-limit value, recompiling only the given translation unit
 # (every pass numbered above the limit that can be skipped is skipped) and
 # linking the product's objects for the rest.  List the numbered passes with
-#   hipcc <HIP_FLAGS> <defines> --offload-device-only -c -o /dev/null <tu> -mllvm -opt-bisect-limit=-1
+#   hipcc <tu_flags(tu)> <defines> --offload-device-only -c -o /dev/null <tu> -mllvm -opt-bisect-limit=-1
 # Usage: tools/bisect_pass.sh <tag> <tu.hip> "<defines>" <limit>...   -> var/bisect_<tag>_<limit>.so
 # (run in this container after `python __graft_entry__.py`; then, on the GPU box,
 #  tools/sink_guard.py wp_crash with PAXISIM_LIB set to each variant)
@@ -11,7 +11,7 @@ set -e -o pipefail
 TAG=$1; TU=$2; DEFS=$3; shift 3
 R=$(cd "$(dirname "$0")/.." && pwd)
 cd "$R"
-FLAGS=$(python3 -c "import __graft_entry__ as g; print(' '.join(g.HIP_FLAGS))")
+FLAGS=$(python3 -c "import __graft_entry__ as g; print(' '.join(g.tu_flags('$TU')))")
 SRCS=$(python3 -c "import __graft_entry__ as g; print(' '.join(g.HIP_SOURCES))")
 SID=$(python3 -c "import __graft_entry__ as g; print(g.source_id())")
 mkdir -p var build/bisect

@@ -10,10 +10,12 @@ OBJ=$R/build/var_$(basename "$OUT" .so)
 mkdir -p "$OBJ" "$(dirname "$R/$OUT")"
 cd "$R"
 SRCS=$(python3 -c "import __graft_entry__ as g; print(' '.join(g.HIP_SOURCES))")
-FLAGS=${BASEFLAGS:-$(python3 -c "import __graft_entry__ as g; print(' '.join(g.HIP_FLAGS))")}
+tuflags() {   # the product's flags of one unit (__graft_entry__.tu_flags), or BASEFLAGS for every unit
+  if [ -n "${BASEFLAGS:-}" ]; then echo "$BASEFLAGS"; else python3 -c "import __graft_entry__ as g; print(' '.join(g.tu_flags('$1')))"; fi
+}
 pids=()
 for s in $SRCS; do
-  /opt/rocm/bin/hipcc $FLAGS "$@" -c -o "$OBJ/${s%.hip}.o" "paxi_amd/csrc/$s" &
+  /opt/rocm/bin/hipcc $(tuflags "$s") "$@" -c -o "$OBJ/${s%.hip}.o" "paxi_amd/csrc/$s" &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait "$p"; done

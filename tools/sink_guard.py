@@ -1,10 +1,11 @@
-"""Run the parity cases that caught LLVM's pre-RA MachineSink miscompile
- on the library PAXISIM_LIB names and print, as one JSON line,
-which of them diverge from the oracle.  tests/test_machine_sink_gpu.py runs it
-on the guard variant (built without -disable-machine-sink) and on the product
-library.
+"""Run the parity cases that caught the kernels' miscompiles (DESIGN.md §5.3:
+round 3's pre-RA MachineSink, round 5's WPaxos absorb variant) on the library
+PAXISIM_LIB names and print, as one JSON line, which of them diverge from the
+oracle.  tests/test_miscompile_guard_gpu.py runs it on the guard variant
+(paxi_amd/guard/libpaxisim_absorb.so) and on the product library;
+tools/bisect_pass.sh's pass-bisection libraries are judged with it too.
 
-  PAXISIM_LIB=paxi_amd/guard/libpaxisim_sink.so python tools/sink_guard.py
+  PAXISIM_LIB=paxi_amd/guard/libpaxisim_absorb.so python tools/sink_guard.py wp_crash
 """
 import json
 import os
