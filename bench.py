@@ -451,6 +451,14 @@ def main():
             "flagged_clusters": {n: int(tot["flag_" + n]) for n in FLAG_NAMES},
             "clusters_total": args.clusters * world,
             "kernel_ms_per_step": kms_max / args.steps,
+            # where a bench step's wall time goes: the step kernel (HIP events on its stream) and the
+            # rest - compaction and phase binning, the statistics, launch gaps; per virtual step a
+            # wave's replica-steps are a chain of dependent HBM round trips (config 1: one wave)
+            "time_split": {"kernel_ms_per_step": kms / args.steps,
+                           "other_ms_per_step": max(0.0, dt - kms / 1e3) / args.steps * 1e3,
+                           "us_per_virtual_step": dt / (args.steps * args.sim_steps) * 1e6,
+                           "kernel_us_per_virtual_step": kms / (args.steps * args.sim_steps) * 1e3,
+                           "msgs_per_virtual_step": tot["delivered_total"] / (args.steps * args.sim_steps)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": f"{kname}<{abi.n_replicas(cfg)},{proto}>",

@@ -510,6 +510,9 @@ __device__ __forceinline__ void fault_process(const Params& P, Rep<NT>& x, uint3
 #ifndef PXS_FLUSH_LATE
 #define PXS_FLUSH_LATE 1
 #endif
+#ifndef PXS_LINK_LATE
+#define PXS_LINK_LATE 1   // the unstaged loop issues its first record load before the link state's (replica_step)
+#endif
 #ifndef PXS_PREFETCH2
 #define PXS_PREFETCH2 0   // 1: unstaged loop loads records two messages ahead (A/B r2l: -13% on config 2, more spills)
 #endif
@@ -576,7 +579,13 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
   x.rw = 0;
   x.hs = step_key(x.kc, x.t);
   if (P.late_workers) client_start<NT>(P, x);
-  {
+  const ScriptedStep sc = P.nfaults ? scripted_scan<NT>(P, x) : ScriptedStep{0u, 0u, 0ull, false};
+  x.crashed = sc.crash;
+  // The random fault process and the step's link masks.  Nothing before the
+  // first handler's sends reads them, so the unstaged loop runs this after it
+  // has issued its first record load: the link state's HBM round trip then
+  // overlaps the record's instead of preceding it (PXS_LINK_LATE).
+  auto link_step = [&]() {
     // link state exists only under a random fault process (without one it stays 0)
     const bool random_faults = P.drop_ppm || P.slow_ppm;
     uint32_t du[Rep<NT>::NL], su[Rep<NT>::NL];
@@ -586,10 +595,10 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
       su[d] = d < N && random_faults ? P.link_slow[krc(P, d, x.r, x.c)] : 0u;
     }
     fault_process<NT>(P, x, du, su);
-    const ScriptedStep sc = P.nfaults ? scripted_scan<NT>(P, x) : ScriptedStep{0u, 0u, 0ull, false};
-    x.crashed = sc.crash;
     link_masks<NT>(P, x, du, su, sc);
-  }
+  };
+  constexpr bool LINK_LATE = !STAGED && PXS_LINK_LATE;
+  if constexpr (!LINK_LATE) link_step();
 
   const uint32_t box0 = (x.b0 * N + x.r) * NS;          // inbox boxes: box0 + src
   // per source: records left (rem) and the step's initial count, packed in
@@ -723,6 +732,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
       m = x.rec[ri];
     }
   }
+  if constexpr (LINK_LATE) link_step();
   while (total && !x.stop) {
 #ifdef PXS_STAMPS
     const unsigned long long w0 = stamp();
