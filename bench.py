@@ -158,7 +158,8 @@ def measured_traffic(args, kernel, mbox, bid):
     bytes in every run, but bytes per launch change along the run (a ~1,200-step
     ramp, then clusters dying), so a record of another window is not attached.
     Counters cannot be read from inside this process."""
-    path = os.path.join(ROOT, "profiles", f"traffic_config{args.config}.json")
+    fz0 = args.config == 4 and getattr(args, "fz", 1) == 0          # the Grid variant has its own record
+    path = os.path.join(ROOT, "profiles", f"traffic_config{args.config}{'_fz0' if fz0 else ''}.json")
     try:
         t = json.load(open(path))
     except (OSError, ValueError):
