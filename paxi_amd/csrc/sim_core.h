@@ -907,7 +907,7 @@ __device__ __forceinline__ void agree_drain(const Params& P, const Rep<NT>& x, u
       const uint32_t k = e.y >> 8;
       // indexed by the cluster, not its slot: compaction does not move the ring
       // (paxisim.hip swap_slots).  Only Multi-Paxos compacts; elsewhere slot ==
-      // cluster, and x.c keeps those kernels' code as it was
+      // cluster and the slot index is used as before
       const uint64_t cl = Proto::kind == PAXISIM_PAXOS && !PXS_AGR_SLOT ? x.gid - P.cluster_base : x.c;
       unsigned long long* a = &P.agr[((size_t)(k % P.AR) * P.NK + e.z) * P.C + cl];
       const unsigned long long v = *a;

@@ -82,6 +82,20 @@ def main():
             for t in range(lo, hi):
                 ph[:, (start + t) % k] += lead[t]
             res[name] = cost(np.lexsort((ph.sum(axis=1), np.argmax(ph, axis=1))), h, T)
+    # what compaction implements (phase binning): classes by
+    # residue, arbitrary order inside a class; and with each class split into
+    # load buckets (quantiles of the previous half-window's records)
+    ph = np.zeros((L, 3))
+    for t in range(0, h):
+        ph[:, (start + t) % 3] += lead[t]
+    cls, load = np.argmax(ph, axis=1), Ml[:h].sum(axis=(0, 2))
+    shuf = rng.permutation(L)
+    res["phase3_binned"] = cost(shuf[np.argsort(cls[shuf], kind="stable")], h, T)
+    for nb in (2, 3, 4):
+        edges = np.quantile(load, np.linspace(0, 1, nb + 1)[1:-1])
+        bucket = np.searchsorted(edges, load, side="right")
+        key = cls * nb + bucket
+        res["phase3_binned_%d_load_buckets" % nb] = cost(shuf[np.argsort(key[shuf], kind="stable")], h, T)
     # replica order per lane: each lane runs its replicas busiest first (the
     # step's counts are known before any replica runs), so the k-th replica-step
     # of every lane in a wave is its k-th busiest; and the bound where lanes
