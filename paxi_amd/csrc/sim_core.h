@@ -92,10 +92,40 @@ __device__ __forceinline__ uint32_t lsel(const uint32_t (&a)[Rep<NT>::NL], uint3
 // socket.Send (socket.go:66-109): crash -> drop -> flaky -> slow, then the
 // bounded (link, arrival-step) bucket.  Returns the record index to write.
 // ---------------------------------------------------------------------------
+// One exit (PXS_SEND_ONE_EXIT, on): the filter's verdict is a value and the
+// drop is counted once at the end.  The early-return form - a return inside
+// the divergent Flaky branch - is the shape LLVM has miscompiled in three
+// builds (a register live across the branch held the Flaky
+// probability, or another stale value, on the dropping lanes' path to the
+// join); with one exit neither reproducer of round 5 diverges
+// (gpurun_out/r5l).  0 keeps the early returns (A/B, reproducers).
+#ifndef PXS_SEND_ONE_EXIT
+#define PXS_SEND_ONE_EXIT 1
+#endif
 template <int NT>
 __device__ __forceinline__ bool send_begin(const Params& P, Rep<NT>& x, uint32_t to, uint32_t nrec, uint32_t& ri) {
   const uint32_t seq = x.send_seq++;
   x.sent++;
+  if constexpr (PXS_SEND_ONE_EXIT) {
+    // crash, unknown id (socket.go:86-88) and drop were folded into dmask at step start
+    bool ok = to < nrep<NT>(P) && !((x.dmask >> to) & 1u);
+    if (ok && ((x.fmask >> to) & 1u)) {                // flaky (socket.go:77-81), scripted only
+      uint32_t p = 0;
+      scripted(P, PAXISIM_FAULT_FLAKY, x.gid, x.r, to, x.t, &p);
+      ok = !ppm_hit(draw(x.hs, tag(PUR_FLAKY, x.r, seq)), p);
+    }
+    uint32_t b = x.b0 + 1u + (uint32_t)((x.dly >> (4u * to)) & 15u);   // slow (socket.go:99-106)
+    if (b >= P.D) b -= P.D;
+    const uint32_t box = (b * nrep<NT>(P) + (ok ? to : 0u)) * P.NS + x.r;
+    const uint32_t k = ok ? (uint32_t)x.l_cnt[(box << 6) | x.lane] : 0u;
+    const bool ovf = ok && k + nrec > P.M;
+    if (ovf) x.flags |= PAXISIM_F_MBOX_OVF | PAXISIM_F_UNFAITHFUL;
+    ok = ok && !ovf;
+    x.dropped += ok ? 0u : 1u;
+    if (ok) x.l_cnt[(box << 6) | x.lane] = (uint8_t)(k + nrec);
+    ri = ((box * P.M + k) << 6) | x.lane;
+    return ok;
+  }
   // crash, unknown id (socket.go:86-88) and drop were folded into dmask at step start
   if (to >= nrep<NT>(P) || ((x.dmask >> to) & 1u)) { x.dropped++; return false; }
   if ((x.fmask >> to) & 1u) {                          // flaky (socket.go:77-81), scripted only
@@ -1209,6 +1239,174 @@ __device__ __forceinline__ void rep_counters_flush(const Params& P, const Rep<NT
   if (x.replies) stat_add(&P.stats[krc(P, ST_REPLIES, r, c)], x.replies);
 }
 
+// ---------------------------------------------------------------------------
+// Lane-asynchronous replica progress (PXS_LANE_ASYNC).  The
+// serial kernel's replica-steps of one step are independent (sends land in
+// later steps' buckets), so a lane need not wait at each replica-step for the
+// wave's busiest lane: here every lane walks its own cluster's replicas
+// (busiest first) and starts the next one as soon as its inbox is drained.
+// A trip handles one message for every lane that has one; starting a
+// replica-step (its registers and inbox counts) and finishing one (write-back,
+// counters) run in divergent branches of the same loop, and starts are batched
+// - taken when PXS_ASYNC_BATCH lanes wait or no lane has a message left - so
+// the wave does not pay a start for every lane that finishes.  Semantics are
+// the replica-step's exactly (replica_step's unstaged path, no absorption).
+// ---------------------------------------------------------------------------
+#ifndef PXS_LANE_ASYNC
+#define PXS_LANE_ASYNC 0
+#endif
+#ifndef PXS_ASYNC_BATCH
+#define PXS_ASYNC_BATCH 16
+#endif
+template <int NT, class Proto>
+__device__ __forceinline__ void step_async(const Params& P, Rep<NT>& x, uint64_t order, bool run, uint8_t* img,
+                                           uint8_t* scr) {
+  constexpr uint32_t NSMAX = NT ? (uint32_t)NT + 1u : (uint32_t)PAXISIM_MAX_N + 1u;
+  constexpr uint32_t NCW = (NSMAX + 3u) / 4u;
+  const uint32_t N = nrep<NT>(P), NS = N + 1u;
+  uint32_t k = run ? 0u : N;            // replica-steps started
+  bool act = false;                     // a replica-step in progress
+  size_t ri0 = 0;                       // rc() of the current replica
+  uint32_t box0 = 0, total = 0, u = 0, i = 0, src = 0, ri = 0;
+  uint4 m = make_uint4(0u, 0u, 0u, 0u);
+  RemT<NSMAX, NT == 9 && PXS_PACKREM9> rem;
+  uint32_t c0w[NCW];
+  rem.clear();
+#pragma unroll
+  for (uint32_t q = 0; q < NCW; q++) c0w[q] = 0;
+  auto pick = [&](uint32_t idx, uint32_t& psrc, uint32_t& pri) {
+    if (!(idx & 1u)) u = draw(x.hs, tag(PUR_ORDER, x.r, idx >> 1));
+    uint32_t pk = (((idx & 1u) ? (u >> 16) : (u & 0xFFFFu)) * total) >> 16;
+    bool found = false;
+    psrc = 0;
+    uint32_t p0 = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < NSMAX; s++) {
+      const uint32_t rs = rem.get(s);
+      const bool here = !found && pk < rs;
+      if (here) { psrc = s; p0 = ((c0w[s >> 2] >> ((s & 3u) * 8u)) & 0xFFu) - rs; found = true; }
+      else if (!found) pk -= rs;
+    }
+    pri = (((box0 + psrc) * P.M + p0) << 6) | x.lane;
+  };
+  // Outer loop: finish the lanes whose replica-step is drained, start the next
+  // one of every lane that has one left; inner loop: merge trips as in
+  // replica_step, until no lane has a message or PXS_ASYNC_BATCH lanes wait.
+  for (;;) {
+    if (act && (total == 0u || x.stop)) {          // replica_step's tail and the serial kernel's write-back
+      act = false;
+      reply_flush<NT>(P, x);
+#pragma unroll
+      for (uint32_t s = 0; s < NSMAX; s++)
+        if (s < NS) x.l_cnt[((box0 + s) << 6) | x.lane] = 0;
+      if (x.stop) atomicMin(&x.l_poison[x.lane], x.t);
+      wb_flush<NT>(x);
+      P.flags[ri0] = x.flags;
+      if (P.kv) P.kv_ver[ri0] = x.kvver;
+      Proto::template store<NT>(P, x);
+      if constexpr (Proto::step_scratch) Proto::template step_end<NT>(P, x);
+      rep_counters_flush<NT>(P, x);
+    }
+    if (!act && k < N) {                              // the lane's next replica, busiest first
+      const uint32_t r = (uint32_t)(order >> (4u * k)) & 15u;
+      k++;
+      act = true;
+      x.r = r;
+      x.ci = ~0u;
+      x.l_a = reinterpret_cast<uint32_t*>(img + P.img.off_a);
+      x.l_b = reinterpret_cast<uint32_t*>(img + P.img.off_b);
+      x.l_c = reinterpret_cast<uint32_t*>(img + P.img.off_c);
+      ri0 = rc(P, r, x.c);
+      x.flags = P.flags[ri0];
+      x.kvver = P.kv ? P.kv_ver[ri0] : 0u;
+      Proto::template load<NT>(P, x);
+      if constexpr (Proto::step_scratch) Proto::template step_begin<NT>(P, x, scr);
+      rep_counters_zero<NT>(x);
+      // replica_step's set-up (unstaged path)
+      x.send_seq = 0;
+      x.stop = false;
+      x.im = 0;
+      x.rw = 0;
+      x.hs = step_key(x.kc, x.t);
+      if (P.late_workers) client_start<NT>(P, x);
+      const ScriptedStep sc = P.nfaults ? scripted_scan<NT>(P, x) : ScriptedStep{0u, 0u, 0ull, false};
+      x.crashed = sc.crash;
+      box0 = (x.b0 * N + r) * NS;
+      rem.clear();
+#pragma unroll
+      for (uint32_t q = 0; q < NCW; q++) c0w[q] = 0;
+      total = 0;
+#pragma unroll
+      for (uint32_t s = 0; s < NSMAX; s++) {
+        if (s < NS) {
+          uint32_t n = x.l_cnt[((box0 + s) << 6) | x.lane];
+          if (x.crashed && s < N && n) {                    // socket.Recv discards (socket.go:111-118)
+            for (uint32_t q = 0; q < n;) {
+              const uint32_t h = ldg(&x.rec[(((box0 + s) * P.M + q) << 6) | x.lane]).x;
+              x.discarded++;
+              q += rec_len(h);
+            }
+            n = 0;
+          }
+          rem.put(s, n);
+          c0w[s >> 2] |= n << ((s & 3u) * 8u);
+          total += n;
+        }
+      }
+      i = 0;
+      if (total) {
+        pick(0, src, ri);
+        m = x.rec[ri];
+      }
+      {   // the link state after the first record load (PXS_LINK_LATE)
+        const bool random_faults = P.drop_ppm || P.slow_ppm;
+        uint32_t du[Rep<NT>::NL], su[Rep<NT>::NL];
+#pragma unroll
+        for (uint32_t d = 0; d < Rep<NT>::NL; d++) {
+          du[d] = d < N && random_faults ? P.link_drop[krc(P, d, x.r, x.c)] : 0u;
+          su[d] = d < N && random_faults ? P.link_slow[krc(P, d, x.r, x.c)] : 0u;
+        }
+        fault_process<NT>(P, x, du, su);
+        link_masks<NT>(P, x, du, su, sc);
+      }
+    }
+    if (!__ballot(act)) break;
+    // merge trips; a lane whose inbox is drained waits here until the batch ends
+    for (;;) {
+      const bool busy = act && total != 0u && !x.stop;
+      const uint64_t bb = __ballot(busy);
+      if (!bb || __popcll(__ballot(!busy && (act || k < N))) >= PXS_ASYNC_BATCH) break;
+      if (busy) {
+        const uint32_t len = rec_len(m.x);
+        rem.sub(src, len);
+        total -= len;
+        uint32_t nsrc = 0, nri = 0;
+        uint4 nm = make_uint4(0u, 0u, 0u, 0u);
+        if (total) {
+          pick(i + 1u, nsrc, nri);
+          nm = x.rec[nri];
+        }
+        if (src == N) {
+          x.client++;
+          Proto::template client_request<NT>(P, x, m.w);
+        } else {
+          Proto::template dispatch<NT>(P, x, src, m, ri);
+        }
+        reply_flush<NT>(P, x);
+        intent_flush<NT>(P, x);
+        src = nsrc;
+        ri = nri;
+        m = nm;
+        i++;
+      }
+    }
+  }
+}
+template <int NT, class Proto> constexpr bool lane_async() {
+  // the busiest-first protocols without same-trip absorption (the merge loop above has none)
+  return PXS_LANE_ASYNC && Proto::kind == PAXISIM_WPAXOS && !PXS_WP_ABSORB;
+}
+
 #ifndef PXS_SERIAL_WAVES_ABD
 #define PXS_SERIAL_WAVES_ABD 3   // ABD's kernels fit 168 VGPRs without spilling
 #endif
@@ -1260,6 +1458,14 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
   for (uint32_t t = t0; t < t0 + nsteps; t++) {
     if (PXS_PHASE_RECENT && P.phase_sort && t == t0 + nsteps / 2u)   // the launch's second half only
       for (uint32_t k = 0; k < P.phase_period; k++) reinterpret_cast<uint32_t*>(x.l_cnt + P.ph_rel)[(k << 6) | x.lane] = 0;
+#ifndef PXS_STAMPS
+    if constexpr (lane_async<NT, Proto>()) {
+      const bool run = live && x.l_poison[x.lane] >= t;
+      x.t = t;
+      x.b0 = b0;
+      step_async<NT, Proto>(P, x, run ? replica_order<NT>(P, x, b0) : 0ull, run, img, L + (P.off_wscr - tail));
+    } else
+#endif
     if (live && x.l_poison[x.lane] >= t) {
       const uint64_t order = busy_first<NT, Proto>() ? replica_order<NT>(P, x, b0) : 0x0FEDCBA987654321ull;
 #pragma nounroll

@@ -8,7 +8,8 @@ created.  Whether the wrong code appears depends on the exact source, so
 build() compiles that unit from a pinned commit (__graft_entry__.GUARD_COMMIT)
 into paxi_amd/guard/libpaxisim_absorb.so, a live reproducer; this test asserts that it diverges from the oracle and that
 the product library does not, on the same case (tools/sink_guard.py), and that
-the variant built without LLVM's SDWA peephole does not either."""
+neither does the variant built without LLVM's SDWA peephole nor the variant
+whose send_begin is the product's one-exit form (the source-level fix)."""
 import json
 import os
 import subprocess
@@ -25,6 +26,7 @@ import __graft_entry__ as ge  # noqa: E402
 def test_guard_variants_are_declared():
     assert ge.GUARDS["absorb"] == ["-DPXS_WP_ABSORB=1", "-mllvm", "-disable-machine-sink"]
     assert ge.GUARDS["absorb_nosdwa"][-1] == "-amdgpu-sdwa-peephole=false"
+    assert ge.GUARDS["absorb_oneexit"] == ge.GUARDS["absorb"] and ge.GUARD_SEND_PATCH == {"absorb_oneexit"}
     assert ge.GUARD_UNIT in ge.HIP_SOURCES
 
 
@@ -53,6 +55,17 @@ def test_absorb_without_sdwa_peephole_matches_oracle():
     """The pass bisection's finding: the same absorb source,
     built without LLVM's SDWA peephole, does not diverge."""
     lib = ge.guard_lib("absorb_nosdwa")
+    assert os.path.exists(os.path.join(ROOT, lib)), "guard variant not built: run __graft_entry__.build()"
+    res = _run(lib, "wp_crash")
+    assert not res["diverged"]["wp_crash"], res
+
+
+@pytest.mark.gpu
+def test_absorb_with_one_exit_send_matches_oracle():
+    """The source-level fix the product ships (sim_core.h PXS_SEND_ONE_EXIT):
+    the pinned reproducer with the tree's one-exit send_begin in place of its
+    early-return one does not diverge, with the same flags as the reproducer."""
+    lib = ge.guard_lib("absorb_oneexit")
     assert os.path.exists(os.path.join(ROOT, lib)), "guard variant not built: run __graft_entry__.build()"
     res = _run(lib, "wp_crash")
     assert not res["diverged"]["wp_crash"], res
