@@ -1172,7 +1172,16 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     zero_bytes = sz.first;
     total = sz.second;
   }
-  hipError_t e = hipMalloc(&h->arena, total);
+  // Arena placement experiments (the two run modes): PAXISIM_ARENA_PAD_MB
+  // reserves that much device memory first and frees it once the arena is placed;
+  // PAXISIM_ARENA_CONTIG=1 asks for physically contiguous memory.  Placement only.
+  void* pad = nullptr;
+  if (const char* ev = getenv("PAXISIM_ARENA_PAD_MB"))
+    if (atoll(ev) > 0) (void)hipMalloc(&pad, (size_t)atoll(ev) << 20);
+  const char* cev = getenv("PAXISIM_ARENA_CONTIG");
+  hipError_t e = cev && atoi(cev) ? hipExtMallocWithFlags(&h->arena, total, hipDeviceMallocContiguous)
+                                  : hipMalloc(&h->arena, total);
+  if (pad) (void)hipFree(pad);
   if (e != hipSuccess) {
     delete h;
     return fail(PAXISIM_ENOMEM, "hipMalloc(%zu bytes) failed: %s", total, hipGetErrorString(e));

@@ -22,6 +22,12 @@ for r in rows:
     if 'sim_steps' not in r['Kernel_Name'] and 'sim_serial' not in r['Kernel_Name']: continue
     agg[int(r['Dispatch_Id'])][r['Counter_Name']]+=float(r['Counter_Value'])
 ds=sorted(agg)[-10:]
-print(' '.join(f"{k}={sum(agg[d][k] for d in ds)/len(ds):.4g}" for k in agg[ds[-1]]), '(mean of the last', len(ds), 'dispatches)')
+import os
+kt=os.path.join(os.path.dirname(sys.argv[1]),'run_kernel_trace.csv')
+dur=''
+if os.path.exists(kt):
+    d={int(r['Dispatch_Id']):(int(r['End_Timestamp'])-int(r['Start_Timestamp']))/1e6 for r in csv.DictReader(open(kt)) if int(r['Dispatch_Id']) in ds}
+    dur=f" kernel_ms={sum(d.values())/max(1,len(d)):.3f}"
+print(' '.join(f"{k}={sum(agg[d][k] for d in ds)/len(ds):.4g}" for k in agg[ds[-1]]) + dur, '(mean of the last', len(ds), 'dispatches)')
 PY
 done
