@@ -1419,6 +1419,9 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
   const uint32_t bound = __builtin_amdgcn_readfirstlane(*P.bound);
   const uint32_t blk = blockIdx.x;
   if ((uint64_t)blk * LANES >= bound) return;
+#ifdef PXS_WAVE_TIMES
+  const uint64_t wt0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz, the same clock on every CU
+#endif
   const uint32_t N = nrep<NT>(P);
   uint8_t* img = P.image + (size_t)blk * P.img.bytes;
   // LDS holds the image tail [tail, bytes) - from the client tables on, or
@@ -1539,6 +1542,13 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
     uint4* g = reinterpret_cast<uint4*>(img + tail);
     for (uint32_t k = threadIdx.x; k < nb; k += LANES) g[k] = lds[k];
   }
+#ifdef PXS_WAVE_TIMES
+  if (threadIdx.x == 0 && P.dbg) {
+    const uint64_t wt1 = __builtin_amdgcn_s_memrealtime();
+    P.dbg[2 * (size_t)blk] = wt0;
+    P.dbg[2 * (size_t)blk + 1] = wt1;
+  }
+#endif
 }
 
 }  // namespace pxs

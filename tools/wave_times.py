@@ -1,0 +1,82 @@
+"""Diagnostic: how well one launch of the serial step kernel fills the GPU
+(PXS_WAVE_TIMES build, var/v_wavetimes.so).  Every live workgroup (one wave,
+64 clusters) records its start and end on the 100 MHz clock; per launch this
+prints the makespan, the busy fraction busy / (slots x makespan) with slots =
+the resident waves the occupancy allows, the tail (time from the first moment
+fewer than `slots` waves run until the end), and the spread of wave durations
+by dispatch order.
+
+  python tools/wave_times.py <config> <warm launches> <launches> [clusters]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from paxi_amd import abi  # noqa: E402
+import bench  # noqa: E402
+
+L = C.CDLL(os.path.join(ROOT, os.environ.get("PAXISIM_WT_LIB", "var/v_wavetimes.so")))
+abi.declare(L, "paxisim")
+L.paxisim_step.argtypes = [C.c_void_p, C.c_uint32]
+L.paxisim_dbg_enable.argtypes = [C.c_void_p]
+L.paxisim_dbg_read.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
+L.paxisim_occupancy.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+
+
+def main():
+    config, warm, launches = (int(a) for a in sys.argv[1:4])
+    d = bench.DEFAULTS[config]
+    clusters = int(sys.argv[4]) if len(sys.argv) > 4 else d["clusters"]
+    a = argparse.Namespace(window=d["window"], mbox=d["mbox"], history=512, kv=1, fz=1, crash_step=5 * d["sim_steps"])
+    cfg, wl, fp, faults, _ = bench.workload(config, clusters, 0, 0, a)
+    S = bench.LAUNCH_DEFAULT.get(config, 50)
+    cfg.steps_per_launch = S
+    h = C.c_void_p()
+    assert L.paxisim_create(C.byref(cfg), C.byref(wl), C.byref(fp) if fp is not None else None, C.byref(h)) == 0, \
+        L.paxisim_last_error()
+    for f in faults:
+        assert L.paxisim_fault_add(h, C.byref(f)) == 0
+    assert L.paxisim_dbg_enable(h) == 0
+    bpc, lds, stg = C.c_int(), C.c_uint32(), C.c_uint32()
+    assert L.paxisim_occupancy(h, C.byref(bpc), C.byref(lds), C.byref(stg)) == 0
+    slots = bpc.value * 256
+    nb = (clusters + 63) // 64
+    buf = (C.c_ulonglong * (nb * 16 * 48))()
+    for _ in range(warm):
+        L.paxisim_step(h, S)
+    L.paxisim_dbg_read(h, buf)
+    out = []
+    for k in range(launches):
+        L.paxisim_step(h, S)
+        L.paxisim_dbg_read(h, buf)
+        t = np.frombuffer(buf, dtype=np.uint64, count=2 * nb).reshape(nb, 2).astype(np.int64)
+        live = t[:, 1] > 0
+        t0, t1 = t[live, 0], t[live, 1]
+        base = t0.min()
+        span = (t1.max() - base) / 100.0                     # us
+        dur = (t1 - t0) / 100.0
+        busy = dur.sum() / (slots * span)
+        ev = np.concatenate([np.stack([t0, np.ones_like(t0)], 1), np.stack([t1, -np.ones_like(t1)], 1)])
+        ev = ev[np.lexsort((ev[:, 1], ev[:, 0]))]
+        run = np.cumsum(ev[:, 1])
+        full = np.nonzero(run >= min(slots, live.sum()))[0]
+        tail_from = ev[full[-1], 0] if len(full) else base
+        q = np.array_split(dur, 4)                             # by dispatch order (block index)
+        rec = {"launch": warm + k, "waves": int(live.sum()), "slots": slots, "makespan_us": round(span, 1),
+               "busy_frac": round(float(busy), 3), "tail_us": round((t1.max() - tail_from) / 100.0, 1),
+               "wave_us_mean": round(float(dur.mean()), 1), "wave_us_max": round(float(dur.max()), 1),
+               "wave_us_by_quarter": [round(float(x.mean()), 1) for x in q],
+               "last_start_us": round((t0.max() - base) / 100.0, 1)}
+        out.append(rec)
+        print(json.dumps(rec), flush=True)
+    L.paxisim_destroy(h)
+
+
+if __name__ == "__main__":
+    main()
