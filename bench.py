@@ -46,10 +46,12 @@ DEFAULTS = {1: dict(clusters=1, sim_steps=3010, window=32, mbox=16),
             3: dict(clusters=1 << 20, sim_steps=80, window=16, mbox=16),
             4: dict(clusters=1 << 19, sim_steps=200, window=16, mbox=24),
             5: dict(clusters=1 << 18, sim_steps=200, window=16, mbox=24)}
-# virtual steps fused per kernel launch: 50, and config 3's whole 80-step bench
-# step in one launch (A/B r4ls2: 44.6 -> 45.8 G msgs/s; configs 2 and 5 are
-# best at 50); PAXISIM_LAUNCH_STEPS overrides
-LAUNCH_DEFAULT = {3: 80}
+# virtual steps per chunk: 50 (configs 2 and 5 are best at 50),
+# config 3 20: its 80-step bench step is one pipelined launch of 4 chunks
+# (A/B r5v: +5.7% against one 80-step launch, itself +2.7%
+# over 50-step launches in round 4); PAXISIM_LAUNCH_STEPS overrides.  The
+# library fuses up to 4 chunks per launch (PAXISIM_PIPE)
+LAUNCH_DEFAULT = {3: 20}
 
 
 def launch_steps(cfg_id):
@@ -414,6 +416,8 @@ def main():
         proto = {3: "AbdProto", 5: wp}.get(args.config, "PaxosProto")
         # the library's default step kernel is the serial one
         kname = "sim_steps" if os.environ.get("PAXISIM_SERIAL") == "0" else "sim_serial"
+        if kname == "sim_serial" and args.steps * args.sim_steps > launches * launch_steps(args.config):
+            kname = "sim_serial_pipe"             # chunks fused into pipelined launches
         occ = sim.occupancy()
         desc.update({"tiles_per_cu": occ[0], "lds_per_tile": occ[1], "staged_msgs": occ[2]})
         desc.update({"clusters_per_gpu": args.clusters, "sim_steps_per_step": args.sim_steps,

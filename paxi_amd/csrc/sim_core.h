@@ -1413,12 +1413,11 @@ template <int NT, class Proto> constexpr bool lane_async() {
 template <class Proto> constexpr int serial_waves() {
   return Proto::kind == PAXISIM_ABD ? PXS_SERIAL_WAVES_ABD : PXS_SERIAL_WAVES;
 }
+// One tile (64 clusters, one wave) through steps [t0, t0 + nsteps): the body of
+// both serial kernels below.
 template <int NT, class Proto>
-__global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Params P, uint32_t t0, uint32_t nsteps) {
-  extern __shared__ uint4 lds[];
-  const uint32_t bound = __builtin_amdgcn_readfirstlane(*P.bound);
-  const uint32_t blk = blockIdx.x;
-  if ((uint64_t)blk * LANES >= bound) return;
+__device__ __forceinline__ void serial_tile(const Params& P, uint32_t blk, uint32_t bound, uint32_t t0, uint32_t nsteps,
+                                            uint4* lds) {
 #ifdef PXS_WAVE_TIMES
   const uint64_t wt0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz, the same clock on every CU
 #endif
@@ -1549,6 +1548,69 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
     P.dbg[2 * (size_t)blk + 1] = wt1;
   }
 #endif
+}
+
+template <int NT, class Proto>
+__global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Params P, uint32_t t0, uint32_t nsteps) {
+  extern __shared__ uint4 lds[];
+  const uint32_t bound = __builtin_amdgcn_readfirstlane(*P.bound);
+  const uint32_t blk = blockIdx.x;
+  if ((uint64_t)blk * LANES >= bound) return;
+  serial_tile<NT, Proto>(P, blk, bound, t0, nsteps, lds);
+}
+
+// The pipelined serial kernel: K chunks of nsteps steps of
+// every live tile in one launch, so a slot freed by a tile that finishes its
+// chunk takes the next ready (tile, chunk) instead of idling until the last
+// wave of the launch ends (config 2 at 2.5 waves per slot: up to 19% idle).
+// Clusters are independent, so the only ordering is a tile's own chunks.
+// Each workgroup (one wave) takes one ticket from its XCD's queue - tile i
+// belongs to XCD i mod 8, tickets chunk-major - so a tile's chunks all run
+// under one L2 and the hand-over needs no L2 write-back: the finishing wave
+// waits for its stores (vmcnt 0) and raises the tile's chunk count; the next
+// chunk's wave polls it and invalidates its L1.  A ticket is taken only by a
+// running wave and waits only on a lower ticket, so every wait ends; a poll
+// that outlives PXS_PIPE_SPIN sets q[8] and leaves, and an XCD given fewer
+// workgroups than tickets leaves chunks unrun, which pipe_verify (paxisim.hip)
+// reports - either way the host fails loudly.  The grid is 8 * ceil(tiles / 8)
+// * K workgroups (the dispatcher deals workgroups to the 8 XCDs in turn).
+// (A persistent form - resident waves looping over tickets - hung on the GPU
+// in round 5, gpurun_out/r5t; not kept.)
+// q: [0, 8) tickets per XCD, [8] error (sticky), [16, 16 + tiles) chunks done.
+#ifndef PXS_PIPE_SPIN
+#define PXS_PIPE_SPIN (1u << 22)   // polls of ~2 us: seconds, against chunks of at most ~0.1 s
+#endif
+template <int NT, class Proto>
+__global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial_pipe(Params P, uint32_t t0, uint32_t nsteps,
+                                                                               uint32_t K, uint32_t* q) {
+  extern __shared__ uint4 lds[];
+  const uint32_t bound = __builtin_amdgcn_readfirstlane(*P.bound);
+  const uint32_t tiles = (bound + LANES - 1u) / LANES;
+  const uint32_t xcd = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((32 - 1) << 11)) & 7u;   // HW_REG_XCC_ID
+  const uint32_t tx = tiles > xcd ? (tiles - xcd + 7u) / 8u : 0u;
+  uint32_t it = 0;
+  if (threadIdx.x == 0) it = atomicAdd(&q[xcd], 1u);
+  it = __builtin_amdgcn_readfirstlane(it);
+  if (it >= tx * K) return;
+  // uniform by construction; said so, so the tile's addressing stays in scalar registers
+  const uint32_t c = __builtin_amdgcn_readfirstlane(it / tx);
+  const uint32_t blk = __builtin_amdgcn_readfirstlane(xcd + 8u * (it - c * tx));
+  uint32_t* done = q + 16;
+  if (c) {
+    uint32_t spins = 0;
+    while (__hip_atomic_load(&done[blk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c) {
+      __builtin_amdgcn_s_sleep(8);
+      if (++spins > PXS_PIPE_SPIN) {
+        if (threadIdx.x == 0) atomicOr(&q[8], 1u);
+        return;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // L1 invalidate: the chunk before ran on another CU
+  }
+  serial_tile<NT, Proto>(P, blk, bound, t0 + c * nsteps, nsteps, lds);
+  __builtin_amdgcn_s_waitcnt(0x0F70);                     // vmcnt(0): the tile's stores are in this XCD's L2
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  if (threadIdx.x == 0) __hip_atomic_store(&done[blk], c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace pxs

@@ -19,6 +19,8 @@ struct StepOps {
   hipError_t (*attrs)(int* vgprs, int* max_threads);
   bool staged;   // the instance carries the LDS-staged merge loop (sim_core.h stage_built)
   bool serial;   // the serial kernel: one wave per tile plays every replica (sim_core.h sim_serial)
+  // serial kernels: K chunks of n steps in one launch (sim_core.h sim_serial_pipe)
+  hipError_t (*launch_pipe)(const Params& P, hipStream_t s, uint32_t t0, uint32_t n, uint32_t K, uint32_t* q);
 };
 
 // defined in k_paxos*.hip, k_abd.hip, k_wpaxos.hip; nullptr launch = not built
@@ -71,10 +73,6 @@ struct SerialInstance {
     sim_serial<NT, Proto><<<(unsigned)(P.C / LANES), LANES, (size_t)P.lds_bytes, s>>>(P, t0, n);
     return hipGetLastError();
   }
-  static hipError_t set_lds(int bytes) {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&sim_serial<NT, Proto>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-  }
   static hipError_t occupancy(const Params& P, int* blocks) {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, reinterpret_cast<const void*>(&sim_serial<NT, Proto>),
                                                         (int)LANES, (size_t)P.lds_bytes);
@@ -88,7 +86,20 @@ struct SerialInstance {
     }
     return e;
   }
-  static StepOps ops() { return StepOps{&launch, &set_lds, &occupancy, &attrs, false, true}; }
+  static hipError_t launch_pipe(const Params& P, hipStream_t s, uint32_t t0, uint32_t n, uint32_t K, uint32_t* q) {
+    const unsigned g = (((unsigned)(P.C / LANES) + 7u) / 8u) * 8u * K;   // one ticket per workgroup
+    sim_serial_pipe<NT, Proto><<<g, LANES, (size_t)P.lds_bytes, s>>>(P, t0, n, K, q);
+    return hipGetLastError();
+  }
+  static hipError_t set_lds(int bytes) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sim_serial<NT, Proto>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sim_serial_pipe<NT, Proto>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    return e;
+  }
+  static StepOps ops() { return StepOps{&launch, &set_lds, &occupancy, &attrs, false, true, &launch_pipe}; }
 };
 #endif
 

@@ -5,8 +5,9 @@ round 5 the round-4 WPaxos same-key P2b absorb (PXS_WP_ABSORB=1) miscompiles
 with the round-4 flags (MachineSink off): at step 2 of the wp_crash case the Flaky ppm
 (200000) of replica 3's P1b send lands in the slot of every instance the P1a
 created.  Whether the wrong code appears depends on the exact source, so
-build() compiles that unit from a pinned commit (__graft_entry__.GUARD_COMMIT)
-into paxi_amd/guard/libpaxisim_absorb.so, a live reproducer; this test asserts that it diverges from the oracle and that
+build() compiles the whole library from a pinned commit (__graft_entry__.GUARD_COMMIT;
+only its C ABI, include/paxisim.h, must equal the tree's) into
+paxi_amd/guard/libpaxisim_absorb.so, a live reproducer; this test asserts that it diverges from the oracle and that
 the product library does not, on the same case (tools/sink_guard.py), and that
 neither does the variant built without LLVM's SDWA peephole nor the variant
 whose send_begin is the product's one-exit form (the source-level fix)."""

@@ -12,7 +12,8 @@ step() {
   echo "$n rc=$rc"; tail -4 "$O/$n.log" | cut -c1-400
   case $rc in 0) return 0 ;; *) echo "stopping after $n"; exit $rc ;; esac
 }
-step wt_c2 300 python tools/wave_times.py 2 40 12
+step wt_c2 300 python tools/wave_times.py 2 40 6
+step wt_c2b 300 python tools/wave_times.py 2 150 4
 step wt_c5 300 python tools/wave_times.py 5 20 8
 step wt_c4 300 python tools/wave_times.py 4 20 8
-step wt_c3 300 python tools/wave_times.py 3 5 6
+

@@ -51,7 +51,7 @@ def main():
     for _ in range(warm):
         L.paxisim_step(h, S)
     L.paxisim_dbg_read(h, buf)
-    out = []
+    out, prev = [], {}
     for k in range(launches):
         L.paxisim_step(h, S)
         L.paxisim_dbg_read(h, buf)
@@ -68,11 +68,30 @@ def main():
         full = np.nonzero(run >= min(slots, live.sum()))[0]
         tail_from = ev[full[-1], 0] if len(full) else base
         q = np.array_split(dur, 4)                             # by dispatch order (block index)
+        def greedy(d):                                         # list scheduling on `slots` wave slots
+            free = np.zeros(min(slots, len(d)))
+            for x in d:
+                i = free.argmin()
+                free[i] += x
+            return free.max()
+        live_blk = np.nonzero(live)[0]
+        order = np.argsort(t0, kind="stable")
+        sim_block = greedy(dur[np.argsort(live_blk, kind="stable")])
+        sim_lpt = greedy(np.sort(dur)[::-1])
+        # longest-predicted-first: the previous launch's duration of the same tile as the prediction
+        pred = np.array([prev.get(int(b), 0.0) for b in live_blk])
+        sim_pred = greedy(dur[np.argsort(-pred, kind="stable")])
+        prev.clear()
+        prev.update({int(b): float(x) for b, x in zip(live_blk, dur)})
         rec = {"launch": warm + k, "waves": int(live.sum()), "slots": slots, "makespan_us": round(span, 1),
                "busy_frac": round(float(busy), 3), "tail_us": round((t1.max() - tail_from) / 100.0, 1),
                "wave_us_mean": round(float(dur.mean()), 1), "wave_us_max": round(float(dur.max()), 1),
                "wave_us_by_quarter": [round(float(x.mean()), 1) for x in q],
-               "last_start_us": round((t0.max() - base) / 100.0, 1)}
+               "last_start_us": round((t0.max() - base) / 100.0, 1), "max_running": int(run.max()),
+               "dispatch_in_block_order": bool(np.all(np.diff(live_blk[order]) > 0)),
+               "model_block_order_us": round(float(sim_block), 1), "model_longest_first_us": round(float(sim_lpt), 1),
+               "model_predicted_first_us": round(float(sim_pred), 1),
+               "duration_corr_prev": round(float(np.corrcoef(pred, dur)[0, 1]), 3) if pred.any() else None}
         out.append(rec)
         print(json.dumps(rec), flush=True)
     L.paxisim_destroy(h)
