@@ -4,7 +4,7 @@ injection per GPU (BASELINE config 2), on 1..8 GPUs.
 
 One bench "step" = one pass of the hot path over the whole batch: every
 cluster of every rank advances --sim-steps virtual steps (config 2: 400, as
-launches of 50 steps each).  With the driver's --warmup 5 --steps 20 the
+chunks of 25 steps, three per pipelined launch between compactions).  With the driver's --warmup 5 --steps 20 the
 timed region is config 2's virtual steps 2,000-10,000: past the ~1,200-step
 ramp while clusters desynchronise, and ending at the config's 10,000 steps.
 Inputs (cluster state, mailboxes) are resident in HBM before the timed region.
@@ -46,12 +46,14 @@ DEFAULTS = {1: dict(clusters=1, sim_steps=3010, window=32, mbox=16),
             3: dict(clusters=1 << 20, sim_steps=80, window=16, mbox=16),
             4: dict(clusters=1 << 19, sim_steps=200, window=16, mbox=24),
             5: dict(clusters=1 << 18, sim_steps=200, window=16, mbox=24)}
-# virtual steps per chunk: 50 (configs 2 and 5 are best at 50),
-# config 3 20: its 80-step bench step is one pipelined launch of 4 chunks
-# (A/B r5v: +5.7% against one 80-step launch, itself +2.7%
-# over 50-step launches in round 4); PAXISIM_LAUNCH_STEPS overrides.  The
-# library fuses up to 4 chunks per launch (PAXISIM_PIPE)
-LAUNCH_DEFAULT = {3: 20}
+# virtual steps per chunk: 50 (config 5 is best at 50 unpipelined, DESIGN.md
+# §5.6); config 2 25, compacted every 3 chunks (+0.9 /
+# +2.2% over 50-step chunks compacted every 100); config 3 20: its 80-step
+# bench step is one pipelined launch of 4 chunks (A/B r5v: +5.7% against one
+# 80-step launch, itself +2.7% over 50-step launches in round 4);
+# PAXISIM_LAUNCH_STEPS overrides.  The library fuses up to 4 chunks per launch
+# (PAXISIM_PIPE)
+LAUNCH_DEFAULT = {2: 25, 3: 20}
 
 
 def launch_steps(cfg_id):

@@ -1221,11 +1221,12 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     // compaction: Paxos (the swap covers its arrays); PAXISIM_COMPACT=0 turns it off (A/B)
     const char* ce = getenv("PAXISIM_COMPACT");
     P.compact = cfg->protocol == PAXISIM_PAXOS && !(ce && atoi(ce) == 0);
-    // pipelined (PAXISIM_PIPE > 1, the default): compaction every two launches' worth of steps, so two
-    // chunks fuse (A/B r5v, config 2: +2.0% against compaction every 50 steps unpipelined; every 100
-    // unpipelined -3.3%, every 200 with four chunks +0.0%)
+    // pipelined (PAXISIM_PIPE > 1, the default): compaction every three chunks (at most pipe_max), so
+    // they fuse (A/B r5v / r5x, config 2: 50-step chunks with compaction every 100 +2.0% against every
+    // 50 unpipelined, every 200 with four chunks +0.0%; 25-step chunks every 75 another +0.9 / +2.2%
+    // in the two run modes, every 50 +0.5 / +1.1%)
     if (const char* pe = getenv("PAXISIM_PIPE")) h->pipe_max = (uint32_t)atoi(pe) ? (uint32_t)atoi(pe) : 1u;
-    if (h->pipe_max > 1 && h->ops.serial && h->ops.launch_pipe) h->cmp_every = 2u * h->S;
+    if (h->pipe_max > 1 && h->ops.serial && h->ops.launch_pipe) h->cmp_every = (h->pipe_max < 3u ? h->pipe_max : 3u) * h->S;
     if (const char* ev = getenv("PAXISIM_COMPACT_EVERY")) h->cmp_every = (uint32_t)atoi(ev) ? (uint32_t)atoi(ev) : 1u;
     for (uint32_t w = 0; w < wl->outstanding; w++)
       if (P.start_step[w] + 1u > h->late_until) h->late_until = P.start_step[w] + 1u;
