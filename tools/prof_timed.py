@@ -15,7 +15,8 @@ steps = int(sys.argv[2])
 if steps == 0:
     steps = int(json.load(open(sys.argv[3]))["roofline"]["launches"])
 d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
-out = {"kernel": rows[-1]["Kernel_Name"], "dispatches": len(d), "timed": steps,
+names = sorted({r["Kernel_Name"] for r in rows[-steps:]})    # pipelined launches mix sim_serial_pipe and sim_serial
+out = {"kernel": names[0] if len(names) == 1 else names, "dispatches": len(d), "timed": steps,
        "rocprof_avg_timed_ms": sum(d[-steps:]) / steps, "rocprof_avg_all_ms": sum(d) / len(d)}
 if len(sys.argv) > 3:
     b = json.load(open(sys.argv[3]))
