@@ -4,7 +4,7 @@ injection per GPU (BASELINE config 2), on 1..8 GPUs.
 
 One bench "step" = one pass of the hot path over the whole batch: every
 cluster of every rank advances --sim-steps virtual steps (config 2: 400, as
-chunks of 25 steps, three per pipelined launch between compactions).  With the driver's --warmup 5 --steps 20 the
+chunks of 20 steps, three per pipelined launch between compactions).  With the driver's --warmup 5 --steps 20 the
 timed region is config 2's virtual steps 2,000-10,000: past the ~1,200-step
 ramp while clusters desynchronise, and ending at the config's 10,000 steps.
 Inputs (cluster state, mailboxes) are resident in HBM before the timed region.
@@ -46,14 +46,15 @@ DEFAULTS = {1: dict(clusters=1, sim_steps=3010, window=32, mbox=16),
             3: dict(clusters=1 << 20, sim_steps=80, window=16, mbox=16),
             4: dict(clusters=1 << 19, sim_steps=200, window=16, mbox=24),
             5: dict(clusters=1 << 18, sim_steps=200, window=16, mbox=24)}
-# virtual steps per chunk: 50 (config 5 is best at 50 unpipelined, DESIGN.md
-# §5.6); config 2 25, compacted every 3 chunks (+0.9 /
-# +2.2% over 50-step chunks compacted every 100); config 3 20: its 80-step
+# virtual steps per chunk: 50 (configs 4 and 5 are best at 50, A/B r5aa);
+# config 2 20, compacted every 3 chunks (DESIGN.md §5.9, A/Bs r5x, r5aa: 25-step
+# chunks every 75 +0.9 / +2.2% over 50-step chunks every 100, 20-step chunks
+# every 60 another +0.8%); config 3 20: its 80-step
 # bench step is one pipelined launch of 4 chunks (A/B r5v: +5.7% against one
 # 80-step launch, itself +2.7% over 50-step launches in round 4);
 # PAXISIM_LAUNCH_STEPS overrides.  The library fuses up to 4 chunks per launch
 # (PAXISIM_PIPE)
-LAUNCH_DEFAULT = {2: 25, 3: 20}
+LAUNCH_DEFAULT = {2: 20, 3: 20}
 
 
 def launch_steps(cfg_id):
@@ -153,7 +154,7 @@ def workload(cfg_id, clusters, base, device, args):
     raise SystemExit(f"unknown config {cfg_id}")
 
 
-def measured_traffic(args, kernel, mbox, bid):
+def measured_traffic(args, kernel, mbox, bid, alg_per_launch=None):
     """HBM bytes per launch from the PMC passes of tools/traffic.sh (committed as
     profiles/traffic_config<c>.json), attached when the record was measured on
     this build (source fingerprint) and this workload (kernel, clusters, window,
@@ -173,6 +174,10 @@ def measured_traffic(args, kernel, mbox, bid):
             and t.get("mbox_cap") == mbox and t.get("build_id") == bid
             and t.get("warmup") == args.warmup and t.get("steps") == args.steps
             and (args.config != 4 or t.get("fz", 1) == getattr(args, "fz", 1)))
+    # the same launch structure (chunk length, chunks per launch): the seeded run's algorithmic
+    # bytes per launch are then identical
+    if same and alg_per_launch is not None and t.get("alg_bytes_per_launch"):
+        same = abs(t["alg_bytes_per_launch"] - alg_per_launch) <= 1e-9 * alg_per_launch
     if not same:
         return None
     return {"bytes_per_launch": t["bytes_per_launch"], "source": os.path.relpath(path, ROOT),
@@ -475,7 +480,7 @@ def main():
             "build_id_of": "the loaded libpaxisim.so (paxisim_build_id)",
             "build_matches_sources": bid == source_id(),
         }
-        tr = measured_traffic(args, out["roofline"]["kernel"], cfg.mbox_cap, bid)
+        tr = measured_traffic(args, out["roofline"]["kernel"], cfg.mbox_cap, bid, out["roofline"]["alg_bytes_per_launch"])
         if tr is not None:
             out["roofline"]["traffic"] = tr["bytes_per_launch"]
             out["roofline"]["traffic_source"] = tr["source"]
