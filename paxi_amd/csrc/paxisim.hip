@@ -67,7 +67,7 @@ struct paxisim {
   uint32_t cmp_every = 50;         // steps between compactions
   // pipelined serial launches (sim_core.h sim_serial_pipe): up to pipe_max chunks of S steps per launch
   uint32_t pipe_max = 4;
-  uint32_t* d_pipe = nullptr;      // [0,8) tickets, [8] error, [16, 16 + C/64) chunks done per tile
+  uint32_t* d_pipe = nullptr;      // [0,8) tickets, [8] error, [16, 16 + max(C/64, 64)) chunks done per tile
   uint32_t last_cmp = 0;
   uint32_t late_until = 0;         // no compaction before every late worker has started
   uint32_t bound_host = 0;         // last bound read back (diagnostics)
@@ -339,6 +339,15 @@ __global__ void check_kernel(Params P, uint64_t* out) {
   }
   bad = wave_sum(bad);
   if ((threadIdx.x & 63) == 0 && bad) atomicAdd((unsigned long long*)out, (unsigned long long)bad);
+}
+
+// Pipelined launches (sim_core.h sim_serial_pipe) need the dispatcher to deal a
+// launch's workgroups to 8 XCDs in turn (any rotation): each XCD's ticket queue
+// then has exactly one workgroup per ticket.  This records the XCD of 64
+// workgroups; create turns pipelining off when they are not dealt that way
+// (another compute partition mode), rather than let chunks go unrun.
+__global__ void xcc_probe(uint32_t* out) {
+  if (threadIdx.x == 0) out[blockIdx.x] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((32 - 1) << 11));   // HW_REG_XCC_ID
 }
 
 // paxisim_inject: one client request record into (bucket b, dst r, src client)
@@ -1221,23 +1230,34 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     // compaction: Paxos (the swap covers its arrays); PAXISIM_COMPACT=0 turns it off (A/B)
     const char* ce = getenv("PAXISIM_COMPACT");
     P.compact = cfg->protocol == PAXISIM_PAXOS && !(ce && atoi(ce) == 0);
+    for (uint32_t w = 0; w < wl->outstanding; w++)
+      if (P.start_step[w] + 1u > h->late_until) h->late_until = P.start_step[w] + 1u;
+    // pipelined launches (serial kernels): PAXISIM_PIPE = chunks per launch at most (1: off; default 4)
+    if (const char* pe = getenv("PAXISIM_PIPE")) h->pipe_max = (uint32_t)atoi(pe) ? (uint32_t)atoi(pe) : 1u;
+    if (h->pipe_max > 1 && h->ops.serial && h->ops.launch_pipe) {
+      uint32_t xcc[64] = {0};
+      const size_t nq = 16 + (C / LANES > 64 ? C / LANES : 64);   // the probe writes 64 words after the header
+      if ((e = hipMalloc(&h->d_pipe, sizeof(uint32_t) * nq)) != hipSuccess ||
+          (e = hipMemsetAsync(h->d_pipe, 0, sizeof(uint32_t) * 16, h->stream)) != hipSuccess)
+        rc1 = fail(PAXISIM_EDEVICE, "pipelined launch setup failed: %s", hipGetErrorString(e));
+      if (!rc1) {
+        xcc_probe<<<64, 64, 0, h->stream>>>(h->d_pipe + 16);
+        if ((e = hipGetLastError()) != hipSuccess ||
+            (e = hipMemcpyAsync(xcc, h->d_pipe + 16, sizeof xcc, hipMemcpyDeviceToHost, h->stream)) != hipSuccess ||
+            (e = hipStreamSynchronize(h->stream)) != hipSuccess)
+          rc1 = fail(PAXISIM_EDEVICE, "XCD probe failed: %s", hipGetErrorString(e));
+        for (uint32_t b = 0; b < 64 && !rc1; b++)     // round robin over 8 XCDs, any rotation
+          if ((xcc[b] & 7u) != ((xcc[0] + b) & 7u) || xcc[b] > 7u) h->pipe_max = 1;
+      }
+    } else {
+      h->pipe_max = 1;
+    }
     // pipelined (PAXISIM_PIPE > 1, the default): compaction every three chunks (at most pipe_max), so
     // they fuse (A/B r5v / r5x, config 2: 50-step chunks with compaction every 100 +2.0% against every
     // 50 unpipelined, every 200 with four chunks +0.0%; 25-step chunks every 75 another +0.9 / +2.2%
     // in the two run modes, every 50 +0.5 / +1.1%)
-    if (const char* pe = getenv("PAXISIM_PIPE")) h->pipe_max = (uint32_t)atoi(pe) ? (uint32_t)atoi(pe) : 1u;
     if (h->pipe_max > 1 && h->ops.serial && h->ops.launch_pipe) h->cmp_every = (h->pipe_max < 3u ? h->pipe_max : 3u) * h->S;
     if (const char* ev = getenv("PAXISIM_COMPACT_EVERY")) h->cmp_every = (uint32_t)atoi(ev) ? (uint32_t)atoi(ev) : 1u;
-    for (uint32_t w = 0; w < wl->outstanding; w++)
-      if (P.start_step[w] + 1u > h->late_until) h->late_until = P.start_step[w] + 1u;
-    // pipelined launches (serial kernels): PAXISIM_PIPE = chunks per launch at most (1: off; default 4)
-    if (h->pipe_max > 1 && h->ops.serial && h->ops.launch_pipe) {
-      if ((e = hipMalloc(&h->d_pipe, sizeof(uint32_t) * (16 + C / LANES))) != hipSuccess ||
-          (e = hipMemsetAsync(h->d_pipe, 0, sizeof(uint32_t) * 16, h->stream)) != hipSuccess)
-        rc1 = fail(PAXISIM_EDEVICE, "pipelined launch setup failed: %s", hipGetErrorString(e));
-    } else {
-      h->pipe_max = 1;
-    }
     const uint32_t b0 = (uint32_t)cfg->clusters;
     h->bound_host = b0;
     e = hipMemcpyAsync(h->d_cmp, &b0, sizeof b0, hipMemcpyHostToDevice, h->stream);
