@@ -6,7 +6,12 @@ the resident waves the occupancy allows, the tail (time from the first moment
 fewer than `slots` waves run until the end), and the spread of wave durations
 by dispatch order.
 
-  python tools/wave_times.py <config> <warm launches> <launches> [clusters]
+  python tools/wave_times.py <config> <warm launches> <launches> [clusters] [chunks]
+
+With chunks > 1 each measured call steps chunks x the chunk length, which the
+library runs as pipelined launches when its build records
+every (tile, chunk) item (the PXS_WAVE_TIMES pipelined variant): the busy
+fraction is then over all items of the call.
 """
 import argparse
 import ctypes as C
@@ -32,7 +37,8 @@ L.paxisim_occupancy.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_ui
 def main():
     config, warm, launches = (int(a) for a in sys.argv[1:4])
     d = bench.DEFAULTS[config]
-    clusters = int(sys.argv[4]) if len(sys.argv) > 4 else d["clusters"]
+    clusters = int(sys.argv[4]) if len(sys.argv) > 4 and int(sys.argv[4]) else d["clusters"]
+    chunks = int(sys.argv[5]) if len(sys.argv) > 5 else 1
     a = argparse.Namespace(window=d["window"], mbox=d["mbox"], history=512, kv=1, fz=1, crash_step=5 * d["sim_steps"])
     cfg, wl, fp, faults, _ = bench.workload(config, clusters, 0, 0, a)
     S = bench.LAUNCH_DEFAULT.get(config, 50)
@@ -47,14 +53,26 @@ def main():
     assert L.paxisim_occupancy(h, C.byref(bpc), C.byref(lds), C.byref(stg)) == 0
     slots = bpc.value * 256
     nb = (clusters + 63) // 64
-    buf = (C.c_ulonglong * (nb * 16 * 48))()
+    buf = (C.c_ulonglong * (nb * 16 * 48))()   # the library's dbg buffer: 768 words per tile
     for _ in range(warm):
         L.paxisim_step(h, S)
     L.paxisim_dbg_read(h, buf)
     out, prev = [], {}
     for k in range(launches):
-        L.paxisim_step(h, S)
+        L.paxisim_step(h, S * chunks)
         L.paxisim_dbg_read(h, buf)
+        if chunks > 1:                                         # every (tile, chunk) item of the call
+            a = np.frombuffer(buf, dtype=np.uint64, count=2 * nb * (chunks + 1)).reshape(chunks + 1, nb, 2).astype(np.int64)
+            piped = (a[1:, :, 1] > 0).any(axis=0)              # slot 0: sim_serial launches (and each tile's last item)
+            t = np.concatenate([a[1:].reshape(-1, 2), a[0][~piped]])
+            t = t[t[:, 1] > 0]
+            dur = (t[:, 1] - t[:, 0]) / 100.0
+            span = (t[:, 1].max() - t[:, 0].min()) / 100.0
+            rec = {"call": warm + k, "items": int(len(t)), "slots": slots, "makespan_us": round(span, 1),
+                   "busy_frac": round(float(dur.sum() / (slots * span)), 3), "item_us_mean": round(float(dur.mean()), 1)}
+            out.append(rec)
+            print(json.dumps(rec), flush=True)
+            continue
         t = np.frombuffer(buf, dtype=np.uint64, count=2 * nb).reshape(nb, 2).astype(np.int64)
         live = t[:, 1] > 0
         t0, t1 = t[live, 0], t[live, 1]
