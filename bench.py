@@ -447,6 +447,8 @@ def main():
             "data": "synthetic (seeded closed-loop workload, PRNG-keyed faults)",
             "config": desc,
             "commits_per_s": tot["commits"] / dt_max,
+            # rank 0's timed-window deliveries by message type (a W=16 / W=64 line pair must agree)
+            "delivered_by_type_rank0": {k: int(v) for k, v in d["delivered"].items() if v},
             "sim_steps_per_s": args.sim_steps * args.steps / dt_max,
             "agreement_violations": int(tot["violations"]),
             "agreement_coverage": {"checkpoints_compared": int(tot["agree_compared"]),

@@ -888,10 +888,7 @@ static T* carve(char*& p, size_t count) {
 
 static int pipe_check(paxisim* h);
 static int flush_events(paxisim* h) {
-  if (!h->evs.empty()) {
-    const int rc = pipe_check(h);
-    if (rc) return rc;
-  }
+  const bool any = !h->evs.empty();
   for (auto& e : h->evs) {
     float ms = 0;
     HIPCHK(hipEventSynchronize(e.second));
@@ -901,7 +898,8 @@ static int flush_events(paxisim* h) {
     (void)hipEventDestroy(e.second);
   }
   h->evs.clear();
-  return 0;
+  // after the waits: the error word is read once every timed launch has ended
+  return any ? pipe_check(h) : 0;
 }
 
 extern "C" int paxisim_destroy(paxisim* h) {
@@ -1241,6 +1239,13 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
           (e = hipMemsetAsync(h->d_pipe, 0, sizeof(uint32_t) * 16, h->stream)) != hipSuccess)
         rc1 = fail(PAXISIM_EDEVICE, "pipelined launch setup failed: %s", hipGetErrorString(e));
       if (!rc1) {
+        // the poll limit of a chunk wait (sim_core.h pipe_item); PAXISIM_PIPE_SPIN sets it for tests
+        uint32_t spin = PXS_PIPE_SPIN_DEFAULT;
+        if (const char* se = getenv("PAXISIM_PIPE_SPIN")) spin = (uint32_t)strtoul(se, nullptr, 0);
+        if ((e = hipMemcpyAsync(h->d_pipe + 9, &spin, sizeof spin, hipMemcpyHostToDevice, h->stream)) != hipSuccess)
+          rc1 = fail(PAXISIM_EDEVICE, "pipelined launch setup failed: %s", hipGetErrorString(e));
+      }
+      if (!rc1) {
         xcc_probe<<<64, 64, 0, h->stream>>>(h->d_pipe + 16);
         if ((e = hipGetLastError()) != hipSuccess ||
             (e = hipMemcpyAsync(xcc, h->d_pipe + 16, sizeof xcc, hipMemcpyDeviceToHost, h->stream)) != hipSuccess ||
@@ -1326,13 +1331,21 @@ static hipError_t launch_pipe(paxisim* h, uint32_t t0, uint32_t n, uint32_t K) {
   return hipGetLastError();
 }
 
-// a pipelined launch whose wait gave up (PXS_PIPE_SPIN) left its tiles unstepped: fail loudly
+// a pipelined launch whose wait gave up (q[9], PAXISIM_PIPE_SPIN) left its tiles unstepped: fail loudly
+// The copy is ordered on h->stream (a non-blocking stream: a null-stream
+// hipMemcpy would not wait for the launches in flight), so the word read is
+// the one every earlier launch left.  Every readout entry point calls this
+// first, so no caller gets stats or state of a step that did not fully run.
 static int pipe_check(paxisim* h) {
   if (!h->d_pipe) return 0;
-  uint32_t err = 0;
-  HIPCHK(hipMemcpy(&err, h->d_pipe + 8, sizeof err, hipMemcpyDeviceToHost));
-  return err ? fail(PAXISIM_EDEVICE, "pipelined step launch: %s", (err & 1u) ? "a chunk wait timed out"
-                                                                             : "a tile missed chunks") : 0;
+  uint32_t w[8] = {0};   // q[8..16): error word, spin limit, the first give-up
+  HIPCHK(hipMemcpyAsync(w, h->d_pipe + 8, sizeof w, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (!w[0]) return 0;
+  if (w[0] & 1u)
+    return fail(PAXISIM_EDEVICE, "pipelined step launch: a chunk wait timed out (xcd %u ticket %u tile %u chunk %u: "
+                "done[tile] = %u, xcd tickets taken %u)", w[2], w[3], w[4], w[5], w[6], w[7]);
+  return fail(PAXISIM_EDEVICE, "pipelined step launch: a tile missed chunks");
 }
 
 static int compact(paxisim* h) {
@@ -1405,6 +1418,7 @@ extern "C" int paxisim_read_client(paxisim* h, uint64_t cluster, paxisim_worker_
   if (!h || !n_out || (cap && !out)) return fail(PAXISIM_EINVAL, "null argument");
   if (cluster >= h->cfg.clusters) return fail(PAXISIM_ERANGE, "bad cluster");
   HIPCHK(hipSetDevice(h->cfg.device));
+  if (const int rc = pipe_check(h)) return rc;   // results only of launches that fully ran
   const uint32_t n = h->P.WK;
   *n_out = n;
   if (!cap || !n) return 0;
@@ -1439,6 +1453,7 @@ extern "C" int paxisim_read_kv(paxisim* h, uint64_t cluster, uint32_t replica, u
   if (h->P.protocol != PAXISIM_ABD && !h->P.kv) return fail(PAXISIM_EUNSUPP, "replicas keep no Database (config.kv = 0)");
   if (n == 0) return 0;
   HIPCHK(hipSetDevice(h->cfg.device));
+  if (const int rc = pipe_check(h)) return rc;   // results only of launches that fully ran
   uint32_t* d = nullptr;
   HIPCHK(hipMalloc(&d, n * sizeof(uint32_t)));
   read_kv_kernel<<<(n + 63) / 64, 64, 0, h->stream>>>(h->P, cluster, replica, n, d);
@@ -1453,6 +1468,7 @@ extern "C" int paxisim_read_kv(paxisim* h, uint64_t cluster, uint32_t replica, u
 extern "C" int paxisim_active_clusters(paxisim* h, uint64_t* active) {
   if (!h || !active) return fail(PAXISIM_EINVAL, "null argument");
   HIPCHK(hipSetDevice(h->cfg.device));
+  if (const int rc = pipe_check(h)) return rc;   // results only of launches that fully ran
   uint32_t bound = 0;
   HIPCHK(hipMemcpyAsync(&bound, h->d_cmp + CM_BOUND, 4, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -1488,6 +1504,7 @@ extern "C" int paxisim_read_activity(paxisim* h, uint64_t lo, uint64_t n, uint32
   if (lo + n > h->cfg.clusters || lo + n < lo) return fail(PAXISIM_ERANGE, "cluster range");
   if (n == 0) return 0;
   HIPCHK(hipSetDevice(h->cfg.device));
+  if (const int rc = pipe_check(h)) return rc;   // results only of launches that fully ran
   uint32_t* d = nullptr;
   HIPCHK(hipMalloc(&d, n * sizeof(uint32_t)));
   activity_kernel<<<(unsigned)((n + 255) / 256), 256, 0, h->stream>>>(h->P, lo, n, d);
@@ -1587,6 +1604,7 @@ extern "C" int paxisim_read_inbox(paxisim* h, uint64_t cluster, uint32_t replica
   if (!h || !n_out || (cap && !out)) return fail(PAXISIM_EINVAL, "null argument");
   if (cluster >= h->cfg.clusters || replica >= h->P.N) return fail(PAXISIM_ERANGE, "bad inbox");
   HIPCHK(hipSetDevice(h->cfg.device));
+  if (const int rc = pipe_check(h)) return rc;   // results only of launches that fully ran
   HIPCHK(hipStreamSynchronize(h->stream));
   const uint32_t maxn = h->P.NS * h->P.M;   // a bucket set holds at most this many
   paxisim_inbox_record* d = nullptr;
@@ -1611,6 +1629,7 @@ extern "C" int paxisim_commands(paxisim* h, uint64_t cluster, const uint32_t* ci
   if (cluster >= h->cfg.clusters) return fail(PAXISIM_ERANGE, "bad cluster");
   if (n == 0) return 0;
   HIPCHK(hipSetDevice(h->cfg.device));
+  if (const int rc = pipe_check(h)) return rc;   // results only of launches that fully ran
   uint32_t* d = nullptr;
   HIPCHK(hipMalloc(&d, 3ull * n * sizeof(uint32_t)));
   hipError_t e = hipMemcpyAsync(d, cids, n * sizeof(uint32_t), hipMemcpyHostToDevice, h->stream);
@@ -1662,6 +1681,7 @@ extern "C" int paxisim_read_log(paxisim* h, uint64_t cluster, uint32_t replica, 
   if (cluster >= h->cfg.clusters || replica >= h->P.N || key >= h->P.NK) return fail(PAXISIM_ERANGE, "bad entry");
   if (n == 0) return 0;
   HIPCHK(hipSetDevice(h->cfg.device));
+  if (const int rc = pipe_check(h)) return rc;   // results only of launches that fully ran
   paxisim_log_entry* d = nullptr;
   HIPCHK(hipMalloc(&d, n * sizeof(paxisim_log_entry)));
   read_log_kernel<<<(n + 63) / 64, 64, 0, h->stream>>>(h->P, cluster, replica, key, slot_lo, n, d);
@@ -1677,6 +1697,7 @@ extern "C" int paxisim_read_log(paxisim* h, uint64_t cluster, uint32_t replica, 
 extern "C" int paxisim_stats_get(paxisim* h, paxisim_stats* out) {
   if (!h || !out) return fail(PAXISIM_EINVAL, "null argument");
   HIPCHK(hipSetDevice(h->cfg.device));
+  if (const int rc = pipe_check(h)) return rc;   // results only of launches that fully ran
   uint64_t red[NRED];
   HIPCHK(hipMemsetAsync(h->d_scratch, 0, sizeof(uint64_t) * NRED, h->stream));
   stats_kernel<<<(unsigned)(h->P.C / 256 + 1), 256, 0, h->stream>>>(h->P, h->d_scratch);
@@ -1708,6 +1729,7 @@ extern "C" int paxisim_read_state(paxisim* h, uint64_t lo, uint64_t n, paxisim_r
   if (lo + n > h->cfg.clusters || lo + n < lo) return fail(PAXISIM_ERANGE, "cluster range");
   if (n == 0) return 0;
   HIPCHK(hipSetDevice(h->cfg.device));
+  if (const int rc = pipe_check(h)) return rc;   // results only of launches that fully ran
   const size_t cnt = (size_t)n * h->P.N;
   paxisim_replica_state* d = nullptr;
   HIPCHK(hipMalloc(&d, cnt * sizeof(paxisim_replica_state)));
@@ -1726,6 +1748,7 @@ extern "C" int paxisim_read_instances(paxisim* h, uint64_t lo, uint64_t n, paxis
   if (lo + n > h->cfg.clusters || lo + n < lo) return fail(PAXISIM_ERANGE, "cluster range");
   if (n == 0) return 0;
   HIPCHK(hipSetDevice(h->cfg.device));
+  if (const int rc = pipe_check(h)) return rc;   // results only of launches that fully ran
   const uint32_t ni = h->P.protocol == PAXISIM_EPAXOS ? h->P.N * h->P.N : h->P.NI;   // per cluster; EPaxos: (replica, owner log)
   const size_t cnt = (size_t)n * ni;
   paxisim_instance_state* d = nullptr;
@@ -1743,6 +1766,7 @@ extern "C" int paxisim_read_instances(paxisim* h, uint64_t lo, uint64_t n, paxis
 extern "C" int paxisim_check(paxisim* h, uint64_t* violations) {
   if (!h || !violations) return fail(PAXISIM_EINVAL, "null argument");
   HIPCHK(hipSetDevice(h->cfg.device));
+  if (const int rc = pipe_check(h)) return rc;   // results only of launches that fully ran
   HIPCHK(hipMemsetAsync(h->d_scratch, 0, sizeof(uint64_t), h->stream));
   check_kernel<<<(unsigned)(h->P.C / 256 + 1), 256, 0, h->stream>>>(h->P, h->d_scratch);
   HIPCHK(hipGetLastError());
@@ -1773,6 +1797,7 @@ extern "C" int paxisim_history(paxisim* h, uint64_t cluster, uint32_t* buf, uint
   if (!h || !n_out) return fail(PAXISIM_EINVAL, "null argument");
   if (cluster >= h->cfg.clusters) return fail(PAXISIM_ERANGE, "cluster");
   HIPCHK(hipSetDevice(h->cfg.device));
+  if (const int rc = pipe_check(h)) return rc;   // results only of launches that fully ran
   HIPCHK(hipStreamSynchronize(h->stream));   // step kernels run on the non-blocking h->stream
   const Params& P = h->P;
   std::vector<uint32_t> len(P.N);
@@ -1825,6 +1850,7 @@ extern "C" int paxisim_linearizable(paxisim* h, uint64_t* anomalies, uint64_t* o
   if (h->P.protocol != PAXISIM_ABD || h->P.H == 0)
     return fail(PAXISIM_EUNSUPP, "linearizability scan needs protocol ABD with history > 0");
   HIPCHK(hipSetDevice(h->cfg.device));
+  if (const int rc = pipe_check(h)) return rc;   // results only of launches that fully ran
   HIPCHK(hipStreamSynchronize(h->stream));
   const Params& P = h->P;
   // clusters per launch: each gets a stage of N*H ops (its history grouped by key).

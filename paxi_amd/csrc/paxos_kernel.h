@@ -6,7 +6,9 @@
 //
 // Paxos state during a launch:
 //   registers: ballot, slot, execute, active, phase-1 acks, pending/forward counts, digest
-//   LDS:       log window {ballot, cmd|flags, acks} as [r][W][lane] u32 (regions a, b, c)
+//   log window {ballot, cmd|flags, acks} as [r][W][lane] u32 (regions a, b, c of
+//              the tile image): in the HBM image for the serial kernels (the
+//              product, sim_serial*), in LDS for the rounds-1-2 sim_steps kernel
 //   HBM:       request side table, pending/forward tables, digest checkpoints
 #pragma once
 #include "sim_core.h"
@@ -14,7 +16,7 @@
 namespace pxs {
 
 // ---------------------------------------------------------------------------
-// log window in LDS: entry of slot s of replica r at [(r*W + (s & (W-1)))*64 + lane]
+// log window (HBM image, or LDS in sim_steps): entry of slot s of replica r at [(r*W + (s & (W-1)))*64 + lane]
 // ---------------------------------------------------------------------------
 struct Ent { uint32_t b, c, a; };
 

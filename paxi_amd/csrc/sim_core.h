@@ -114,7 +114,9 @@ __device__ __forceinline__ bool send_begin(const Params& P, Rep<NT>& x, uint32_t
       scripted(P, PAXISIM_FAULT_FLAKY, x.gid, x.r, to, x.t, &p);
       ok = !ppm_hit(draw(x.hs, tag(PUR_FLAKY, x.r, seq)), p);
     }
-    uint32_t b = x.b0 + 1u + (uint32_t)((x.dly >> (4u * to)) & 15u);   // slow (socket.go:99-106)
+    // slow (socket.go:99-106); `to & 15` keeps the shift defined for an unknown id,
+    // whose bucket is never written
+    uint32_t b = x.b0 + 1u + (uint32_t)((x.dly >> (4u * (to & 15u))) & 15u);
     if (b >= P.D) b -= P.D;
     const uint32_t box = (b * nrep<NT>(P) + (ok ? to : 0u)) * P.NS + x.r;
     const uint32_t k = ok ? (uint32_t)x.l_cnt[(box << 6) | x.lane] : 0u;
@@ -1568,18 +1570,71 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial(Param
 // belongs to XCD i mod 8, tickets chunk-major - so a tile's chunks all run
 // under one L2 and the hand-over needs no L2 write-back: the finishing wave
 // waits for its stores (vmcnt 0) and raises the tile's chunk count; the next
-// chunk's wave polls it and invalidates its L1.  A ticket is taken only by a
-// running wave and waits only on a lower ticket, so every wait ends; a poll
-// that outlives PXS_PIPE_SPIN sets q[8] and leaves, and an XCD given fewer
-// workgroups than tickets leaves chunks unrun, which pipe_verify (paxisim.hip)
-// reports - either way the host fails loudly.  The grid is 8 * ceil(tiles / 8)
-// * K workgroups (the dispatcher deals workgroups to the 8 XCDs in turn).
-// (A persistent form - resident waves looping over tickets - hung on the GPU
-// in round 5, gpurun_out/r5t; not kept.)
-// q: [0, 8) tickets per XCD, [8] error (sticky), [16, 16 + tiles) chunks done.
-#ifndef PXS_PIPE_SPIN
-#define PXS_PIPE_SPIN (1u << 22)   // polls of ~2 us: seconds, against chunks of at most ~0.1 s
+// chunk's wave polls it and invalidates its L1.
+//
+// Liveness: a ticket is taken only by a wave that is running, and the wave
+// holding ticket j waits only for ticket j - tx (the same tile's previous
+// chunk), which was taken earlier, so by a wave that is running or done; by
+// induction on j every wait ends, whatever the dispatcher makes resident.
+// A poll that outlives the spin limit (q[9], PAXISIM_PIPE_SPIN) sets q[8],
+// records the first stuck wait in q[10..15] and leaves, and an XCD given
+// fewer workgroups than tickets leaves chunks unrun, which pipe_verify
+// (paxisim.hip) reports - either way the host fails loudly at its next call.
+// The grid is 8 * ceil(tiles / 8) * K workgroups (the dispatcher deals
+// workgroups to the 8 XCDs in turn).
+//
+// PXS_PIPE_PERSIST (off): the persistent form, a grid of the
+// resident slots whose waves loop over tickets.  Round 5's first version of it
+// hung on the GPU (gpurun_out/r5t) and its source was not kept; this is the
+// form rebuilt to find out why (tools/pipe_persist.sh).
+// q: [0, 8) tickets per XCD, [8] error (sticky), [9] spin limit,
+//    [10, 16) the first give-up: xcd, ticket, tile, chunk, done[tile], q[xcd];
+//    [16, 16 + tiles) chunks done.
+#ifndef PXS_PIPE_PERSIST
+#define PXS_PIPE_PERSIST 0
 #endif
+#define PXS_PIPE_SPIN_DEFAULT (1u << 22)   // polls of ~2 us: seconds, against chunks of at most ~0.1 s
+template <int NT, class Proto>
+__device__ __forceinline__ bool pipe_item(const Params& P, uint32_t t0, uint32_t nsteps, uint32_t K, uint32_t* q,
+                                          uint32_t bound, uint32_t xcd, uint32_t tx, uint32_t spin_max, uint4* lds) {
+  uint32_t it = 0;
+  if (threadIdx.x == 0) it = atomicAdd(&q[xcd], 1u);
+  it = __builtin_amdgcn_readfirstlane(it);
+  if (it >= tx * K) return false;
+  // uniform by construction; said so, so the tile's addressing stays in scalar registers
+  const uint32_t c = __builtin_amdgcn_readfirstlane(it / tx);
+  const uint32_t blk = __builtin_amdgcn_readfirstlane(xcd + 8u * (it - c * tx));
+  uint32_t* done = q + 16;
+  if (c) {
+    uint32_t spins = 0;
+    uint32_t seen;
+    while ((seen = __hip_atomic_load(&done[blk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < c) {
+      __builtin_amdgcn_s_sleep(8);
+      if (++spins > spin_max) {
+        if (threadIdx.x == 0 && atomicOr(&q[8], 1u) == 0u) {   // the first give-up names its wait
+          q[10] = xcd;
+          q[11] = it;
+          q[12] = blk;
+          q[13] = c;
+          q[14] = seen;
+          q[15] = __hip_atomic_load(&q[xcd], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return false;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // L1 invalidate: the chunk before ran on another CU
+  }
+  serial_tile<NT, Proto>(P, blk, bound, t0 + c * nsteps, nsteps, lds);
+  // the tile's stores must be issued before the wait and the wait before the
+  // flag: the fence keeps the compiler from moving a store past the waitcnt
+  // (the intrinsic is not a memory barrier to LLVM)
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0x0F70);                     // vmcnt(0): the tile's stores are in this XCD's L2
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  if (threadIdx.x == 0) __hip_atomic_store(&done[blk], c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
 template <int NT, class Proto>
 __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial_pipe(Params P, uint32_t t0, uint32_t nsteps,
                                                                                uint32_t K, uint32_t* q) {
@@ -1588,29 +1643,14 @@ __global__ void __launch_bounds__(LANES, serial_waves<Proto>()) sim_serial_pipe(
   const uint32_t tiles = (bound + LANES - 1u) / LANES;
   const uint32_t xcd = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((32 - 1) << 11)) & 7u;   // HW_REG_XCC_ID
   const uint32_t tx = tiles > xcd ? (tiles - xcd + 7u) / 8u : 0u;
-  uint32_t it = 0;
-  if (threadIdx.x == 0) it = atomicAdd(&q[xcd], 1u);
-  it = __builtin_amdgcn_readfirstlane(it);
-  if (it >= tx * K) return;
-  // uniform by construction; said so, so the tile's addressing stays in scalar registers
-  const uint32_t c = __builtin_amdgcn_readfirstlane(it / tx);
-  const uint32_t blk = __builtin_amdgcn_readfirstlane(xcd + 8u * (it - c * tx));
-  uint32_t* done = q + 16;
-  if (c) {
-    uint32_t spins = 0;
-    while (__hip_atomic_load(&done[blk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c) {
-      __builtin_amdgcn_s_sleep(8);
-      if (++spins > PXS_PIPE_SPIN) {
-        if (threadIdx.x == 0) atomicOr(&q[8], 1u);
-        return;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // L1 invalidate: the chunk before ran on another CU
+  const uint32_t spin_max = __builtin_amdgcn_readfirstlane(q[9]);
+  if constexpr (PXS_PIPE_PERSIST) {
+    // every iteration takes a new ticket, so a wave runs at most tx * K items (a bound, not a guess)
+    for (uint32_t n = 0; n <= tx * K; n++)
+      if (!pipe_item<NT, Proto>(P, t0, nsteps, K, q, bound, xcd, tx, spin_max, lds)) break;
+  } else {
+    pipe_item<NT, Proto>(P, t0, nsteps, K, q, bound, xcd, tx, spin_max, lds);
   }
-  serial_tile<NT, Proto>(P, blk, bound, t0 + c * nsteps, nsteps, lds);
-  __builtin_amdgcn_s_waitcnt(0x0F70);                     // vmcnt(0): the tile's stores are in this XCD's L2
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  if (threadIdx.x == 0) __hip_atomic_store(&done[blk], c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace pxs

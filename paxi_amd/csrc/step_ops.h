@@ -87,7 +87,16 @@ struct SerialInstance {
     return e;
   }
   static hipError_t launch_pipe(const Params& P, hipStream_t s, uint32_t t0, uint32_t n, uint32_t K, uint32_t* q) {
-    const unsigned g = (((unsigned)(P.C / LANES) + 7u) / 8u) * 8u * K;   // one ticket per workgroup
+    unsigned g = (((unsigned)(P.C / LANES) + 7u) / 8u) * 8u * K;   // one ticket per workgroup
+    if (PXS_PIPE_PERSIST) {   // the persistent form: the resident slots, a multiple of 8 (sim_core.h)
+      int dev = 0, cus = 0, per = 0;
+      hipError_t e = hipGetDevice(&dev);
+      if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (e == hipSuccess) e = occupancy(P, &per);
+      if (e != hipSuccess) return e;
+      const unsigned slots = ((unsigned)(cus * per) + 7u) / 8u * 8u;
+      if (slots && slots < g) g = slots;
+    }
     sim_serial_pipe<NT, Proto><<<g, LANES, (size_t)P.lds_bytes, s>>>(P, t0, n, K, q);
     return hipGetLastError();
   }

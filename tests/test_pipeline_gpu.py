@@ -70,3 +70,24 @@ def test_abd_pipelined_matches_oracle(monkeypatch):
     assert g.linearizable()[:2] == o.linearizable()[:2]   # (anomalies, ops); the GPU adds partitions skipped
     assert k4 == 2 + 1, k4                                 # 80 = 2 x 4 chunks, 40 = 1 x 4
     g.close()
+
+
+def test_gave_up_wait_fails_every_readout(monkeypatch):
+    """A chunk wait that gives up leaves its tile unstepped; the library must
+    say so at the next call of every kind, never return partial stats or state
+    (ADVICE r5).  PAXISIM_PIPE_SPIN=0 makes the first unsatisfied poll give up:
+    with one tile the waves of chunks 1..K-1 start while chunk 0 runs."""
+    from paxi_amd.sim import PaxisimError, Simulation
+    cfg = abi.make_config(npz=[5], clusters=64, seed=11, window=16, mbox_cap=32, max_delay=4,
+                          steps_per_launch=20)
+    wl = abi.make_workload(outstanding=8, target=0)
+    monkeypatch.setenv("PAXISIM_PIPE", "4")
+    monkeypatch.setenv("PAXISIM_PIPE_SPIN", "0")
+    g = Simulation(cfg, wl)
+    g.step(400)
+    for name, call in [("sync", g.sync), ("stats", g.stats), ("read_state", g.read_state),
+                       ("kernel_time", g.kernel_time), ("check", g.check)]:
+        with pytest.raises(PaxisimError, match="chunk wait timed out") as e:
+            call()
+        assert "done[tile]" in str(e.value), name      # the stuck wait names itself
+    g.close()

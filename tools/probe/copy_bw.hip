@@ -1,62 +1,115 @@
 // copy_bw: the achievable HBM bandwidth of this MI355X (SURVEY.md §8d asks
 // for it beside the 8 TB/s spec peak the roofline fraction is priced on).
-// A grid-stride uint4 copy between two 4 GiB buffers, 256 threads a block,
-// 8 x 256 CUs of blocks; bytes = read + write.  Prints one JSON line.
+// Round 5's verdict: the round-2 form (a grid-stride uint4 loop, one load in
+// flight per thread) measured 4.90 TB/s copy, below the guide's 6.29 TB/s
+// float4 copy (MI355X_MICROARCH.md:36).  This form follows the guide's shape:
+// a float4 (16 B per lane) copy in which every thread has U independent
+// loads in flight before its stores, one pass over the buffer (no grid-stride
+// loop), nontemporal or default-policy loads and stores, buffers of 4 and
+// 16 GiB.  Bytes = read + write.  Prints one JSON line with every variant and
+// the best.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/probe/copy_bw tools/probe/copy_bw.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 
-__global__ void copy_kernel(const uint4* __restrict__ a, uint4* __restrict__ b, size_t n) {
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) b[i] = a[i];
+typedef float f4 __attribute__((ext_vector_type(4)));   // float4 as a clang vector (the nontemporal builtins take it)
+
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) copy_kernel(const f4* __restrict__ a, f4* __restrict__ b, size_t n) {
+  // block k covers [k * 256 * U, (k + 1) * 256 * U): U coalesced 4-KB rows per block
+  const size_t base = (size_t)blockIdx.x * 256u * U + threadIdx.x;
+  f4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const size_t i = base + (size_t)u * 256u;
+    if (i < n) v[u] = NT ? __builtin_nontemporal_load(a + i) : a[i];
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const size_t i = base + (size_t)u * 256u;
+    if (i < n) {
+      if (NT) __builtin_nontemporal_store(v[u], b + i);
+      else b[i] = v[u];
+    }
+  }
 }
 
-__global__ void read_kernel(const uint4* __restrict__ a, size_t n, unsigned* out) {
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  unsigned acc = 0;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint4 v = a[i];
-    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) read_kernel(const f4* __restrict__ a, size_t n, unsigned* out) {
+  const size_t base = (size_t)blockIdx.x * 256u * U + threadIdx.x;
+  float acc = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const size_t i = base + (size_t)u * 256u;
+    if (i < n) {
+      const f4 v = NT ? __builtin_nontemporal_load(a + i) : a[i];
+      acc += v.x + v.y + v.z + v.w;
+    }
   }
-  if (acc == 0x12345678u) out[0] = acc;   // keeps the loads
+  if (acc == 1234.5f) out[0] = 1u;   // keeps the loads
 }
 
 #define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
 
-int main() {
-  const size_t bytes = 4ull << 30, n = bytes / sizeof(uint4);
-  uint4 *a = nullptr, *b = nullptr;
-  unsigned* o = nullptr;
-  CHK(hipMalloc(&a, bytes));
-  CHK(hipMalloc(&b, bytes));
-  CHK(hipMalloc(&o, 4));
-  CHK(hipMemset(a, 1, bytes));
-  CHK(hipMemset(b, 0, bytes));
-  int cus = 0;
-  CHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  const unsigned grid = (unsigned)cus * 8u, block = 256;
+template <int U, bool NT>
+static int run(const f4* a, f4* b, unsigned* o, size_t n, float* best_copy, float* best_read) {
+  const unsigned grid = (unsigned)((n + 256u * U - 1) / (256u * U));
   hipEvent_t e0, e1;
   CHK(hipEventCreate(&e0));
   CHK(hipEventCreate(&e1));
-  float best_copy = 1e30f, best_read = 1e30f;
+  *best_copy = *best_read = 1e30f;
   for (int rep = 0; rep < 12; rep++) {
     float ms = 0;
     CHK(hipEventRecord(e0));
-    copy_kernel<<<grid, block>>>(a, b, n);
+    copy_kernel<U, NT><<<grid, 256>>>(a, b, n);
     CHK(hipEventRecord(e1));
     CHK(hipEventSynchronize(e1));
     CHK(hipEventElapsedTime(&ms, e0, e1));
-    if (rep >= 2 && ms < best_copy) best_copy = ms;
+    if (rep >= 2 && ms < *best_copy) *best_copy = ms;
     CHK(hipEventRecord(e0));
-    read_kernel<<<grid, block>>>(a, n, o);
+    read_kernel<U, NT><<<grid, 256>>>(a, n, o);
     CHK(hipEventRecord(e1));
     CHK(hipEventSynchronize(e1));
     CHK(hipEventElapsedTime(&ms, e0, e1));
-    if (rep >= 2 && ms < best_read) best_read = ms;
+    if (rep >= 2 && ms < *best_read) *best_read = ms;
   }
-  printf("{\"probe\": \"copy_bw\", \"cus\": %d, \"buffer_bytes\": %zu, \"copy_GBps\": %.1f, \"read_GBps\": %.1f, "
-         "\"copy_ms\": %.3f, \"read_ms\": %.3f, \"method\": \"best of 10 timed launches (2 warm-up), uint4 grid-stride, "
-         "bytes = read + write for copy\"}\n",
-         cus, bytes, 2.0 * bytes / (best_copy * 1e6), (double)bytes / (best_read * 1e6), best_copy, best_read);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return 0;
+}
+
+int main() {
+  const size_t max_bytes = 16ull << 30;
+  f4 *a = nullptr, *b = nullptr;
+  unsigned* o = nullptr;
+  CHK(hipMalloc(&a, max_bytes));
+  CHK(hipMalloc(&b, max_bytes));
+  CHK(hipMalloc(&o, 4));
+  CHK(hipMemset(a, 1, max_bytes));
+  CHK(hipMemset(b, 0, max_bytes));
+  printf("{\"probe\": \"copy_bw\", \"method\": \"float4 copy, U loads in flight per thread before its stores, "
+         "one pass, best of 10 timed launches (2 warm-up); bytes = read + write for copy\", \"variants\": [");
+  double best = 0, best_read = 0;
+  const char* sep = "";
+  for (size_t bytes : {4ull << 30, 16ull << 30}) {
+    const size_t n = bytes / sizeof(f4);
+    struct { int u; bool nt; } cases[] = {{1, false}, {4, false}, {8, false}, {4, true}, {8, true}};
+    for (auto c : cases) {
+      float cm = 0, rm = 0;
+      int rc = 0;
+      if (c.u == 1) rc = c.nt ? run<1, true>(a, b, o, n, &cm, &rm) : run<1, false>(a, b, o, n, &cm, &rm);
+      else if (c.u == 4) rc = c.nt ? run<4, true>(a, b, o, n, &cm, &rm) : run<4, false>(a, b, o, n, &cm, &rm);
+      else rc = c.nt ? run<8, true>(a, b, o, n, &cm, &rm) : run<8, false>(a, b, o, n, &cm, &rm);
+      if (rc) return rc;
+      const double cg = 2.0 * bytes / (cm * 1e6), rg = (double)bytes / (rm * 1e6);
+      if (cg > best) best = cg;
+      if (rg > best_read) best_read = rg;
+      printf("%s{\"buffer_bytes\": %zu, \"loads_in_flight\": %d, \"nontemporal\": %s, \"copy_GBps\": %.1f, "
+             "\"read_GBps\": %.1f, \"copy_ms\": %.3f, \"read_ms\": %.3f}",
+             sep, bytes, c.u, c.nt ? "true" : "false", cg, rg, cm, rm);
+      sep = ", ";
+    }
+  }
+  printf("], \"copy_GBps\": %.1f, \"read_GBps\": %.1f}\n", best, best_read);
   return 0;
 }
