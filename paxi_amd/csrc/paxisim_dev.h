@@ -424,4 +424,41 @@ __device__ __forceinline__ size_t krc(const Params& P, uint32_t k, uint32_t r, u
   return ((size_t)k * P.N + r) * P.C + c;
 }
 
+// ---- diagnostic build (PXS_TALLY): the HBM requests of each
+// access class.  At every instrumented load or store the active lanes count
+// the distinct 128-B lines (loads) or 32-B sectors (stores) their addresses
+// fall in - the requests the instruction sends to L2 (a
+// scattered read is one 128-B request, a scattered 16- or 32-B write one 32-B
+// one) - and the first active lane adds (lane accesses, units) to the block's
+// words in P.dbg, loads and stores apart.  tools/tally.py turns them into bytes per message. ----
+enum TallyClass : uint32_t {
+  TC_REC_LD, TC_REC_ST, TC_INST_LD, TC_INST_ST, TC_ENT_LD, TC_ENT_ST, TC_ROW_LD, TC_ROW_ST, TC_CNT, TC_KV_LD,
+  TC_KV_ST, TC_FWD, TC_PEND, TC_CKPT, TC_AGREE, TC_REPLY, TC_GHOST, TC_LINK, TC_OTHER, TC_N
+};
+#ifdef PXS_TALLY
+constexpr uint32_t TALLY_PER = 48;   // = DBG_PER; a block's 16 x 48 words in P.dbg hold [class][load, store][lanes, units]
+__device__ __noinline__ void tally_at(unsigned long long* dbg, uint32_t blk, uint32_t cls, const void* p, bool store) {
+  if (!dbg) return;
+  const unsigned long long unit = (unsigned long long)(uintptr_t)p >> (store ? 5 : 7);
+  unsigned long long m = __ballot(1);
+  const unsigned long long lanes = __popcll(m);
+  const int first = __ffsll((long long)m) - 1;
+  unsigned long long n = 0;
+  while (m) {
+    const int f = __ffsll((long long)m) - 1;
+    const unsigned long long u0 = __shfl(unit, f);
+    m &= ~__ballot(unit == u0);
+    n++;
+  }
+  if ((int)(threadIdx.x & 63u) == first) {
+    unsigned long long* q = &dbg[(size_t)blk * 16 * TALLY_PER + 4 * cls + (store ? 2 : 0)];
+    atomicAdd(&q[0], lanes);
+    atomicAdd(&q[1], n);
+  }
+}
+#define PXS_TALLY_AT(P, blk, cls, ptr, st) tally_at((P).dbg, (blk), (cls), (const void*)(ptr), (st))
+#else
+#define PXS_TALLY_AT(P, blk, cls, ptr, st)
+#endif
+
 }  // namespace pxs

@@ -20,6 +20,13 @@ namespace pxs {
 // ---------------------------------------------------------------------------
 struct Ent { uint32_t b, c, a; };
 
+// PXS_TALLY (paxisim_dev.h): the handlers below see only x
+#ifdef PXS_TALLY
+#define PXS_TALLY_X(x, cls, ptr, st) tally_at((x).tdbg, (x).blk, (cls), (const void*)(ptr), (st))
+#else
+#define PXS_TALLY_X(x, cls, ptr, st)
+#endif
+
 // Two layouts share these handlers.  Multi-Paxos keeps each replica's window
 // in LDS as three u32 planes (l_a / l_b / l_c, entry stride es = 64 lanes) and
 // the request side table in HBM (reqx).  The per-key instances of WPaxos keep
@@ -37,6 +44,7 @@ __device__ __forceinline__ bool hbm_log(const Rep<NT>& x) { return x.es == 4u; }
 template <int NT>
 __device__ __forceinline__ void ecache(Rep<NT>& x, uint32_t i) {
   if (x.ci != i) {
+    PXS_TALLY_X(x, TC_ENT_LD, x.l_a + i, false);
     x.ce = *reinterpret_cast<const uint4*>(x.l_a + i);
     x.ci = i;
   }
@@ -44,21 +52,25 @@ __device__ __forceinline__ void ecache(Rep<NT>& x, uint32_t i) {
 template <int NT>
 __device__ __forceinline__ uint32_t ea(Rep<NT>& x, uint32_t i) {
   if (hbm_log(x)) { ecache(x, i); return x.ce.x; }
+  PXS_TALLY_X(x, TC_ENT_LD, x.l_a + i, false);
   return x.l_a[i];
 }
 template <int NT>
 __device__ __forceinline__ uint32_t eb(Rep<NT>& x, uint32_t i) {
   if (hbm_log(x)) { ecache(x, i); return x.ce.y; }
+  PXS_TALLY_X(x, TC_ENT_LD, x.l_b + i, false);
   return x.l_b[i];
 }
 template <int NT>
 __device__ __forceinline__ uint32_t ec(Rep<NT>& x, uint32_t i) {
   if (hbm_log(x)) { ecache(x, i); return x.ce.z; }
   if (wb_on(x) && x.ci == i) return x.ce.z;
+  PXS_TALLY_X(x, TC_ENT_LD, x.l_c + i, false);
   return x.l_c[i];
 }
 template <int NT>
 __device__ __forceinline__ void set_a(Rep<NT>& x, uint32_t i, uint32_t v) {
+  PXS_TALLY_X(x, TC_ENT_ST, x.l_a + i, true);
   if (hbm_log(x)) { x.l_a[i] = v; if (x.ci == i) x.ce.x = v; return; }
   x.l_a[i] = v;
 }
@@ -71,11 +83,13 @@ __device__ __forceinline__ void cm_note(Rep<NT>& x, uint32_t i, uint32_t c) {
 }
 template <int NT>
 __device__ __forceinline__ void set_b(Rep<NT>& x, uint32_t i, uint32_t v) {
+  PXS_TALLY_X(x, TC_ENT_ST, hbm_log(x) ? x.l_a + i + 1u : x.l_b + i, true);
   if (hbm_log(x)) { x.l_a[i + 1u] = v; if (x.ci == i) x.ce.y = v; cm_note(x, i, v); return; }
   x.l_b[i] = v;
 }
 template <int NT>
 __device__ __forceinline__ void set_c(Rep<NT>& x, uint32_t i, uint32_t v) {
+  PXS_TALLY_X(x, TC_ENT_ST, hbm_log(x) ? x.l_a + i + 2u : x.l_c + i, true);
   if (hbm_log(x)) { x.l_a[i + 2u] = v; if (x.ci == i) x.ce.z = v; return; }
   if (wb_on(x)) {
     if (x.ci != i) wb_flush(x);
@@ -91,6 +105,7 @@ template <int NT>
 __device__ __forceinline__ void eput(Rep<NT>& x, uint32_t i, const Ent& e) {
   if (hbm_log(x)) {                                  // one 12-B store
     uint32_t* q = x.l_a + i;
+    PXS_TALLY_X(x, TC_ENT_ST, q, true);
     *reinterpret_cast<uint2*>(q) = make_uint2(e.b, e.c);
     q[2] = e.a;
     if (x.ci == i) { x.ce.x = e.b; x.ce.y = e.c; x.ce.z = e.a; }
@@ -98,6 +113,9 @@ __device__ __forceinline__ void eput(Rep<NT>& x, uint32_t i, const Ent& e) {
     return;
   }
   if (wb_on(x) && x.ci == i) x.ci = ~0u;            // superseded by this write
+  PXS_TALLY_X(x, TC_ENT_ST, x.l_a + i, true);
+  PXS_TALLY_X(x, TC_ENT_ST, x.l_b + i, true);
+  PXS_TALLY_X(x, TC_ENT_ST, x.l_c + i, true);
   x.l_a[i] = e.b;
   x.l_b[i] = e.c;
   x.l_c[i] = e.a;
@@ -106,10 +124,12 @@ __device__ __forceinline__ void eput(Rep<NT>& x, uint32_t i, const Ent& e) {
 template <int NT>
 __device__ __forceinline__ uint32_t rq_get(Rep<NT>& x, uint32_t i) {
   if (hbm_log(x)) { ecache(x, i); return x.ce.w; }
+  PXS_TALLY_X(x, TC_OTHER, &x.reqx[i], false);
   return ldg(&x.reqx[i]);
 }
 template <int NT>
 __device__ __forceinline__ void rq_set(Rep<NT>& x, uint32_t i, uint32_t q) {
+  PXS_TALLY_X(x, hbm_log(x) ? TC_ENT_ST : TC_OTHER, hbm_log(x) ? x.l_a + i + 3u : &x.reqx[i], true);
   if (hbm_log(x)) { x.l_a[i + 3u] = q; if (x.ci == i) x.ce.w = q; return; }
   x.reqx[i] = q;
 }
@@ -156,12 +176,19 @@ template <int NT>
 __device__ __forceinline__ uint32_t fwd_find(const Params& P, const Rep<NT>& x, uint32_t cid) {
   if (!hbm_log(x)) {                                     // (A/B r2: the LDS-window kernels keep one probe per trip)
     uint32_t i = 0;
-    for (; i < x.nfwd; i++)
+    for (; i < x.nfwd; i++) {
+      PXS_TALLY_AT(P, x.blk, TC_FWD, &P.fwd[krc(P, i, x.r, x.c)], false);
       if (req_cid(ldg(&P.fwd[krc(P, i, x.r, x.c)])) == cid) break;
+    }
     return i;
   }
   for (uint32_t i = 0; i < x.nfwd; i += 4u) {
     uint32_t f[4];
+#ifdef PXS_TALLY
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; k++)
+      if (i + k < x.nfwd) PXS_TALLY_AT(P, x.blk, TC_FWD, &P.fwd[krc(P, i + k, x.r, x.c)], false);
+#endif
 #pragma unroll
     for (uint32_t k = 0; k < 4u; k++) f[k] = i + k < x.nfwd ? P.fwd[krc(P, i + k, x.r, x.c)] : 0u;
 #pragma unroll
@@ -177,8 +204,12 @@ __device__ __forceinline__ void node_forward(const Params& P, Rep<NT>& x, uint32
   const uint32_t i = fwd_find<NT>(P, x, cid);
   if (i == x.nfwd) {
     if (x.nfwd == FMAX) x.flags |= PAXISIM_F_PEND_OVF | PAXISIM_F_UNFAITHFUL;
-    else P.fwd[krc(P, x.nfwd++, x.r, x.c)] = req;
+    else {
+      PXS_TALLY_AT(P, x.blk, TC_FWD, &P.fwd[krc(P, x.nfwd, x.r, x.c)], true);
+      P.fwd[krc(P, x.nfwd++, x.r, x.c)] = req;
+    }
   } else {
+    PXS_TALLY_AT(P, x.blk, TC_FWD, &P.fwd[krc(P, i, x.r, x.c)], true);
     P.fwd[krc(P, i, x.r, x.c)] = req;
   }
   post_unicast<NT>(P, x, to, PAXISIM_MSG_REQUEST, 0u, 0u, cid);
@@ -195,6 +226,11 @@ __device__ __forceinline__ void handle_reply(const Params& P, Rep<NT>& x, uint32
     const uint32_t last = x.nfwd - 1u;
     for (uint32_t i0 = 0; i0 < x.nfwd; i0 += 4u) {
       uint32_t f[4];
+#ifdef PXS_TALLY
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; k++)
+      if (i0 + k < x.nfwd) PXS_TALLY_AT(P, x.blk, TC_FWD, &P.fwd[krc(P, i0 + k, x.r, x.c)], false);
+#endif
 #pragma unroll
       for (uint32_t k = 0; k < 4u; k++) f[k] = i0 + k < x.nfwd ? P.fwd[krc(P, i0 + k, x.r, x.c)] : 0u;
 #pragma unroll
@@ -203,8 +239,12 @@ __device__ __forceinline__ void handle_reply(const Params& P, Rep<NT>& x, uint32
         uint32_t lv = 0;
 #pragma unroll
         for (uint32_t q = 0; q < 4u; q++) lv = last == i0 + q ? f[q] : lv;
-        if (last >= i0 + 4u) lv = ldg(&P.fwd[krc(P, last, x.r, x.c)]);
+        if (last >= i0 + 4u) {
+          PXS_TALLY_AT(P, x.blk, TC_FWD, &P.fwd[krc(P, last, x.r, x.c)], false);
+          lv = ldg(&P.fwd[krc(P, last, x.r, x.c)]);
+        }
         x.nfwd = last;
+        PXS_TALLY_AT(P, x.blk, TC_FWD, &P.fwd[krc(P, i0 + k, x.r, x.c)], true);
         P.fwd[krc(P, i0 + k, x.r, x.c)] = lv;
         request_reply<NT>(P, x, f[k], cid, value);
         return;
@@ -218,6 +258,9 @@ __device__ __forceinline__ void handle_reply(const Params& P, Rep<NT>& x, uint32
     x.flags |= PAXISIM_F_UNFAITHFUL;
     return;
   }
+  PXS_TALLY_AT(P, x.blk, TC_FWD, &P.fwd[krc(P, i, x.r, x.c)], false);
+  PXS_TALLY_AT(P, x.blk, TC_FWD, &P.fwd[krc(P, x.nfwd, x.r, x.c)], false);
+  PXS_TALLY_AT(P, x.blk, TC_FWD, &P.fwd[krc(P, i, x.r, x.c)], true);
   const uint32_t req = ldg(&P.fwd[krc(P, i, x.r, x.c)]);
   x.nfwd--;
   P.fwd[krc(P, i, x.r, x.c)] = ldg(&P.fwd[krc(P, x.nfwd, x.r, x.c)]);
@@ -251,8 +294,9 @@ __device__ __forceinline__ void raise_win(Rep<NT>& x, uint32_t f) {
 // serial (ldg): eight in flight at once would cost 32 registers.
 template <int NT>
 __device__ __forceinline__ uint4* gref(const Params& P, const Rep<NT>& x, uint32_t g) {
-  if (hbm_log(x)) return &P.gst[((size_t)x.inst * P.C + x.c) * GMAX + g];
-  return &P.gst[((size_t)g * P.NI + x.inst) * P.C + x.c];
+  uint4* q = hbm_log(x) ? &P.gst[((size_t)x.inst * P.C + x.c) * GMAX + g] : &P.gst[((size_t)g * P.NI + x.inst) * P.C + x.c];
+  PXS_TALLY_AT(P, x.blk, TC_GHOST, q, false);   // (every use of a ghost reference counted as a line)
+  return q;
 }
 template <int NT>
 __device__ __forceinline__ uint32_t ghost_find(const Params& P, Rep<NT>& x, int32_t s, uint4& e) {
@@ -332,7 +376,10 @@ __device__ __forceinline__ bool in_window(const Params& P, const Rep<NT>& x, int
 
 template <int NT>
 __device__ __forceinline__ void paxos_forward(const Params& P, Rep<NT>& x) {     // paxos.go:371-376
-  for (uint32_t i = 0; i < x.npend; i++) node_forward<NT>(P, x, bal_id(x.ballot), ldg(&x.pend[(size_t)i * x.pstride]));
+  for (uint32_t i = 0; i < x.npend; i++) {
+    PXS_TALLY_AT(P, x.blk, TC_PEND, &x.pend[(size_t)i * x.pstride], false);
+    node_forward<NT>(P, x, bal_id(x.ballot), ldg(&x.pend[(size_t)i * x.pstride]));
+  }
   x.npend = 0;
 }
 
@@ -372,7 +419,10 @@ template <int NT>
 __device__ __forceinline__ void paxos_handle_request(const Params& P, Rep<NT>& x, uint32_t req) {  // paxos.go:86-97
   if (!x.active) {
     if (x.npend == PMAX) x.flags |= PAXISIM_F_PEND_OVF | PAXISIM_F_UNFAITHFUL;
-    else x.pend[(size_t)x.npend++ * x.pstride] = req;
+    else {
+      PXS_TALLY_AT(P, x.blk, TC_PEND, &x.pend[(size_t)x.npend * x.pstride], true);
+      x.pend[(size_t)x.npend++ * x.pstride] = req;
+    }
     if (bal_id(x.ballot) != x.r) paxos_p1a<NT>(P, x);
   } else {
     paxos_p2a<NT>(P, x, req);
@@ -412,11 +462,13 @@ template <int NT>
 __device__ __forceinline__ uint32_t kv_get(const Params& P, Rep<NT>& x, uint32_t key) {
   if (!PXS_REPLY_VALUE) return 0u;
   const uint32_t* a = &P.kv_val[((size_t)key * nrep<NT>(P) + x.r) * P.C + x.c];
+  PXS_TALLY_AT(P, x.blk, TC_KV_LD, a, false);
   return PXS_KV_LDG ? ldg(a) : *a;
 }
 template <int NT>
 __device__ __forceinline__ void kv_exec(const Params& P, Rep<NT>& x, uint32_t h, uint32_t key, uint32_t cmd) {
   if (!wl_write_h(P, h)) return;
+  PXS_TALLY_AT(P, x.blk, TC_KV_ST, &P.kv_val[((size_t)key * nrep<NT>(P) + x.r) * P.C + x.c], true);
   P.kv_val[((size_t)key * nrep<NT>(P) + x.r) * P.C + x.c] = cmd;
   x.kvver++;
 }
@@ -431,6 +483,7 @@ __device__ __forceinline__ void kv_exec(const Params& P, Rep<NT>& x, uint32_t h,
 template <int NT>
 __device__ __forceinline__ void digest_need(const Params& P, Rep<NT>& x) {
   if (hbm_log(x) && P.wlds && x.dig_st == 0u) {
+    PXS_TALLY_AT(P, x.blk, TC_CKPT, &P.wdig[wp_si(P, x.blk, x.key, x.r, x.lane)], false);
     x.digest = P.wdig[wp_si(P, x.blk, x.key, x.r, x.lane)];
     x.dig_st = 1u;
   }
@@ -469,6 +522,8 @@ __device__ __forceinline__ void paxos_exec(const Params& P, Rep<NT>& x, uint32_t
     if ((uint32_t)x.execute % CKI == 0) {
       const uint32_t k = ((uint32_t)x.execute / CKI) % CKR;
       const size_t ci = ((size_t)k * P.NI + x.inst) * P.C + x.c;
+      PXS_TALLY_AT(P, x.blk, TC_CKPT, &P.ck_e[ci], true);
+      PXS_TALLY_AT(P, x.blk, TC_CKPT, &P.ck_d[ci], true);
       P.ck_e[ci] = (uint32_t)x.execute;
       P.ck_d[ci] = x.digest;
       if (P.AR && PXS_AGREE_POST) agree_post<NT>(P, x, (uint32_t)x.execute / CKI);
@@ -494,11 +549,13 @@ __device__ __forceinline__ void paxos_handle_p1a(const Params& P, Rep<NT>& x, ui
   uint32_t ri;
   intent_flush<NT>(P, x);                                                    // keep per-link order
   if (!send_begin<NT>(P, x, bal_id(mb), 1u + n, ri)) return;
+  PXS_TALLY_AT(P, x.blk, TC_REC_ST, &x.rec[ri], true);
   x.rec[ri] = make_uint4(PAXISIM_MSG_P1B | (n << 8) | x.ktag, x.ballot, 0u, 0u);
   for (int32_t s = x.execute; s <= hi; s++) {
     const Ent e = eget<NT>(x, eidx<NT>(P, x, s));
     if (!(e.c & EF_EXISTS) || (e.c & EF_COMMIT)) continue;
     ri += LANES;
+    PXS_TALLY_AT(P, x.blk, TC_REC_ST, &x.rec[ri], true);
     x.rec[ri] = make_uint4(PAXISIM_MSG_P1B_ENTRY, e.b, (uint32_t)s, e.c & CMD_MASK);
   }
 }
@@ -509,6 +566,7 @@ __device__ __forceinline__ void paxos_handle_p1b(const Params& P, Rep<NT>& x, ui
                                               uint32_t n) {                   // paxos.go:164-230
   if (mb < x.ballot || x.active) return;
   for (uint32_t k = 0; k < n; k++) {                                          // update(): 164-180
+    PXS_TALLY_AT(P, x.blk, TC_REC_LD, &x.rec[ri0 + (k + 1u) * LANES], false);
     const uint4 cb = ldg(&x.rec[ri0 + (k + 1u) * LANES]);
     const int32_t s = (int32_t)cb.z;
     if (s > x.slot) x.slot = s;
@@ -551,7 +609,10 @@ __device__ __forceinline__ void paxos_handle_p1b(const Params& P, Rep<NT>& x, ui
       }
       const uint32_t np = x.npend;
       x.npend = 0;
-      for (uint32_t k = 0; k < np; k++) paxos_p2a<NT>(P, x, ldg(&x.pend[(size_t)k * x.pstride]));
+      for (uint32_t k = 0; k < np; k++) {
+        PXS_TALLY_AT(P, x.blk, TC_PEND, &x.pend[(size_t)k * x.pstride], false);
+        paxos_p2a<NT>(P, x, ldg(&x.pend[(size_t)k * x.pstride]));
+      }
     }
   }
 }
@@ -712,6 +773,15 @@ struct PaxosProto {
   template <int NT>
   __device__ static __forceinline__ void load(const Params& P, Rep<NT>& x) {
     const size_t i = rc(P, x.r, x.c);
+#ifdef PXS_TALLY
+    PXS_TALLY_AT(P, x.blk, TC_ROW_LD, &P.ballot[i], false);
+    PXS_TALLY_AT(P, x.blk, TC_ROW_LD, &P.slot[i], false);
+    PXS_TALLY_AT(P, x.blk, TC_ROW_LD, &P.execute[i], false);
+    PXS_TALLY_AT(P, x.blk, TC_ROW_LD, &P.meta[i], false);
+    PXS_TALLY_AT(P, x.blk, TC_ROW_LD, &P.npend[i], false);
+    PXS_TALLY_AT(P, x.blk, TC_ROW_LD, &P.nfwd[i], false);
+    PXS_TALLY_AT(P, x.blk, TC_ROW_LD, &P.digest[i], false);
+#endif
     x.ballot = P.ballot[i];
     x.slot = (int32_t)P.slot[i];
     x.execute = (int32_t)P.execute[i];
@@ -735,6 +805,15 @@ struct PaxosProto {
   template <int NT>
   __device__ static __forceinline__ void store(const Params& P, const Rep<NT>& x) {
     const size_t i = rc(P, x.r, x.c);
+#ifdef PXS_TALLY
+    PXS_TALLY_AT(P, x.blk, TC_ROW_ST, &P.ballot[i], true);
+    PXS_TALLY_AT(P, x.blk, TC_ROW_ST, &P.slot[i], true);
+    PXS_TALLY_AT(P, x.blk, TC_ROW_ST, &P.execute[i], true);
+    PXS_TALLY_AT(P, x.blk, TC_ROW_ST, &P.meta[i], true);
+    PXS_TALLY_AT(P, x.blk, TC_ROW_ST, &P.npend[i], true);
+    PXS_TALLY_AT(P, x.blk, TC_ROW_ST, &P.nfwd[i], true);
+    PXS_TALLY_AT(P, x.blk, TC_ROW_ST, &P.digest[i], true);
+#endif
     P.ballot[i] = x.ballot;
     P.slot[i] = (uint32_t)x.slot;
     P.execute[i] = (uint32_t)x.execute;

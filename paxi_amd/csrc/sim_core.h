@@ -24,6 +24,7 @@ struct Rep {
   uint32_t ballot;
   int32_t slot, execute;
   uint32_t active, p1mask, flags, npend, nfwd;
+  uint32_t nfwd0;                       // WPaxos: nfwd as loaded (the row is written back only if it changed)
   uint64_t digest;
   // the bound Paxos instance (Multi-Paxos: the replica's one; WPaxos: one kpaxos per key)
   uint32_t inst;                        // instance index in [NI] tables (key * N + r)
@@ -52,6 +53,9 @@ struct Rep {
   uint32_t *l_a, *l_b, *l_c, *l_wcur, *l_wiss, *l_poison;
   uint8_t* l_cnt;
   uint8_t* l_agn;                       // agreement-ring arrivals this step, [parity][r][lane] (agree_post)
+#ifdef PXS_TALLY
+  unsigned long long* tdbg;             // PXS_TALLY: P.dbg, for the handlers that only see x
+#endif
   uint32_t* l_inst;                     // WPaxos (wlds): instance scalars in LDS (wpaxos_kernel.h)
   uint32_t ikst, iro;                   // WPaxos (wlds): word offsets of key k / this replica in l_inst
   uint32_t dig_st;                      // WPaxos (wlds): bound instance's digest 0 not loaded, 1 loaded, 2 changed
@@ -218,7 +222,10 @@ template <int NT>
 __device__ __forceinline__ void send1(const Params& P, Rep<NT>& x, uint32_t to, uint32_t w0, uint32_t w1,
                                       uint32_t w2, uint32_t w3) {
   uint32_t ri;
-  if (send_begin<NT>(P, x, to, 1, ri)) x.rec[ri] = make_uint4(w0, w1, w2, w3);
+  if (send_begin<NT>(P, x, to, 1, ri)) {
+    PXS_TALLY_AT(P, x.blk, TC_REC_ST, &x.rec[ri], true);
+    x.rec[ri] = make_uint4(w0, w1, w2, w3);
+  }
 }
 
 // Broadcast: every peer except self, IDs.Less order (socket.go:147-155; G1, G2)
@@ -268,6 +275,7 @@ __device__ __forceinline__ void intent_flush(const Params& P, Rep<NT>& x) {
         continue;
       }
       x.l_cnt[(box << 6) | x.lane] = (uint8_t)(k + 1u);
+      PXS_TALLY_AT(P, x.blk, TC_REC_ST, &x.rec[((box * P.M + k) << 6) | x.lane], true);
       x.rec[((box * P.M + k) << 6) | x.lane] = make_uint4(x.iw0, x.iw1, x.iw2, x.iw3);
     }
     x.im = 0;
@@ -305,6 +313,7 @@ __device__ __forceinline__ void intent_flush(const Params& P, Rep<NT>& x) {
       continue;
     }
     x.l_cnt[(box[d] << 6) | x.lane] = (uint8_t)(k[d] + 1u);
+    PXS_TALLY_AT(P, x.blk, TC_REC_ST, &x.rec[((box[d] * P.M + k[d]) << 6) | x.lane], true);
     x.rec[((box[d] * P.M + k[d]) << 6) | x.lane] = make_uint4(x.iw0, x.iw1, x.iw2, x.iw3);
   }
   x.im = 0;
@@ -425,6 +434,7 @@ __device__ __forceinline__ bool wl_write(const Params& P, uint32_t kc, uint32_t 
 template <int NT>
 __device__ __forceinline__ void reply_flush(const Params& P, Rep<NT>& x) {
   if (x.rw) {
+    PXS_TALLY_AT(P, x.blk, TC_REPLY, &P.wrep[(size_t)(x.rw - 1u) * P.C + x.c], true);
     P.wrep[(size_t)(x.rw - 1u) * P.C + x.c] = x.rv;
     x.rw = 0;
   }
@@ -465,6 +475,7 @@ __device__ __forceinline__ void client_reply(const Params& P, Rep<NT>& x, uint32
       x.flags |= PAXISIM_F_MBOX_OVF | PAXISIM_F_UNFAITHFUL;
       return;
     }
+    PXS_TALLY_AT(P, x.blk, TC_REC_ST, &x.rec[((box * P.M + k) << 6) | x.lane], true);
     x.rec[((box * P.M + k) << 6) | x.lane] = make_uint4(PAXISIM_MSG_REQUEST, 0u, 0u, (uint32_t)nc);
     *cp = (uint8_t)(k + 1u);
   } else {
@@ -511,12 +522,14 @@ __device__ __forceinline__ void fault_process(const Params& P, Rep<NT>& x, uint3
     const uint32_t u = draw(x.hs, tag(PUR_LINK, x.r, d));
     if (P.drop_ppm && x.t >= du[d] && ppm_hit16(u & 0xFFFFu, P.drop_ppm)) {
       du[d] = x.t + P.drop_len;
+      PXS_TALLY_AT(P, x.blk, TC_LINK, &P.link_drop[krc(P, d, x.r, x.c)], true);
       P.link_drop[krc(P, d, x.r, x.c)] = du[d];
     }
     if (P.slow_ppm && x.t >= (su[d] & (T_MAX - 1u)) && ppm_hit16(u >> 16, P.slow_ppm)) {
       const uint32_t span = P.slow_max - P.slow_min + 1u;
       const uint32_t v = draw(x.hs, tag(PUR_SLOWD, x.r, d));
       su[d] = (x.t + P.slow_len) | ((P.slow_min + __umulhi(v, span)) << 28);
+      PXS_TALLY_AT(P, x.blk, TC_LINK, &P.link_slow[krc(P, d, x.r, x.c)], true);
       P.link_slow[krc(P, d, x.r, x.c)] = su[d];
     }
   }
@@ -625,6 +638,12 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
     for (uint32_t d = 0; d < Rep<NT>::NL; d++) {
       du[d] = d < N && random_faults ? P.link_drop[krc(P, d, x.r, x.c)] : 0u;
       su[d] = d < N && random_faults ? P.link_slow[krc(P, d, x.r, x.c)] : 0u;
+#ifdef PXS_TALLY
+      if (d < N && random_faults) {
+        PXS_TALLY_AT(P, x.blk, TC_LINK, &P.link_drop[krc(P, d, x.r, x.c)], false);
+        PXS_TALLY_AT(P, x.blk, TC_LINK, &P.link_slow[krc(P, d, x.r, x.c)], false);
+      }
+#endif
     }
     fault_process<NT>(P, x, du, su);
     link_masks<NT>(P, x, du, su, sc);
@@ -647,6 +666,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
       uint32_t n = x.l_cnt[((box0 + s) << 6) | x.lane];
       if (x.crashed && s < N && n) {                    // socket.Recv discards (socket.go:111-118)
         for (uint32_t k = 0; k < n;) {
+          PXS_TALLY_AT(P, x.blk, TC_REC_LD, &x.rec[(((box0 + s) * P.M + k) << 6) | x.lane], false);
           const uint32_t h = ldg(&x.rec[(((box0 + s) * P.M + k) << 6) | x.lane]).x;
           x.discarded++;
           k += rec_len(h);
@@ -761,6 +781,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
       if (jv) m = stage[0];
       else m = load_now(x.rec + ri);
     } else {
+      PXS_TALLY_AT(P, x.blk, TC_REC_LD, &x.rec[ri], false);
       m = x.rec[ri];
     }
   }
@@ -799,6 +820,7 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
           if (i + 1u < jv) nm = stage[(i + 1u) * LANES];  // staged
           else nm = load_now(x.rec + nri);                // past the stage: a blocking load
         } else {
+          PXS_TALLY_AT(P, x.blk, TC_REC_LD, &x.rec[nri], false);
           nm = x.rec[nri];                                // no stage: one message ahead from HBM
         }
       }
@@ -849,7 +871,10 @@ __device__ __forceinline__ void replica_step(const Params& P, Rep<NT>& x
         } else if (total) {
           pick(i + 1u, nsrc, nri);
           if constexpr (STAGED) nm = i + 1u < jv ? stage[(i + 1u) * LANES] : load_now(x.rec + nri);
-          else nm = x.rec[nri];
+          else {
+            PXS_TALLY_AT(P, x.blk, TC_REC_LD, &x.rec[nri], false);
+            nm = x.rec[nri];
+          }
         }
       }
     }
@@ -919,6 +944,7 @@ __device__ __forceinline__ void agree_post(const Params& P, Rep<NT>& x, uint32_t
   if (n < AGMAX) {
     const uint64_t d = x.digest;
     const uint64_t want = ((uint64_t)k << 40) | ((d ^ (d >> 24)) & 0xFFFFFFFFFFull);
+    PXS_TALLY_AT(P, x.blk, TC_AGREE, &P.agq[(((size_t)par * AGMAX + n) * nrep<NT>(P) + x.r) * P.C + x.c], true);
     P.agq[(((size_t)par * AGMAX + n) * nrep<NT>(P) + x.r) * P.C + x.c] =
         make_uint4((uint32_t)want, (uint32_t)(want >> 32), x.key, 0u);
   }
@@ -934,6 +960,7 @@ __device__ __forceinline__ void agree_drain(const Params& P, const Rep<NT>& x, u
     *cp = 0;
     uint32_t cmp = 0, miss = n > AGMAX ? n - AGMAX : 0u, bad = 0;
     for (uint32_t j = 0; j < n && j < AGMAX; j++) {
+      PXS_TALLY_AT(P, x.blk, TC_AGREE, &P.agq[(((size_t)par * AGMAX + j) * N + r) * P.C + x.c], false);
       const uint4 e = P.agq[(((size_t)par * AGMAX + j) * N + r) * P.C + x.c];
       const unsigned long long want = (unsigned long long)e.x | ((unsigned long long)e.y << 32);
       const uint32_t k = e.y >> 8;
@@ -942,6 +969,7 @@ __device__ __forceinline__ void agree_drain(const Params& P, const Rep<NT>& x, u
       // cluster and the slot index is used as before
       const uint64_t cl = Proto::kind == PAXISIM_PAXOS && !PXS_AGR_SLOT ? x.gid - P.cluster_base : x.c;
       unsigned long long* a = &P.agr[((size_t)(k % P.AR) * P.NK + e.z) * P.C + cl];
+      PXS_TALLY_AT(P, x.blk, TC_AGREE, a, false);
       const unsigned long long v = *a;
       const uint32_t tv = (uint32_t)(v >> 40);
       if (v == 0ull || tv < k) {
@@ -1222,10 +1250,16 @@ __device__ __forceinline__ void rep_counters_zero(Rep<NT>& x) {
 #ifndef PXS_COUNTER_ATOMIC
 #define PXS_COUNTER_ATOMIC 1   // (A/B r3, config 2: +4.9%)
 #endif
-__device__ __forceinline__ void stat_add(uint32_t* p, uint32_t v) {
+#ifdef PXS_TALLY
+#define stat_add(p, v) (PXS_TALLY_AT(P, x.blk, TC_CNT, (p), true), stat_add_((p), (v)))
+#endif
+__device__ __forceinline__ void stat_add_(uint32_t* p, uint32_t v) {
   if (PXS_COUNTER_ATOMIC) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else *p += v;
 }
+#ifndef PXS_TALLY
+#define stat_add stat_add_
+#endif
 template <int NT>
 __device__ __forceinline__ void rep_counters_flush(const Params& P, const Rep<NT>& x) {
   const uint32_t r = x.r;
@@ -1417,6 +1451,37 @@ template <class Proto> constexpr int serial_waves() {
 }
 // One tile (64 clusters, one wave) through steps [t0, t0 + nsteps): the body of
 // both serial kernels below.
+// Idle replica-steps.  A replica whose inbox is empty at a
+// step changes nothing - Paxi has no timers (paxos/paxos.go), and with no
+// message there is no handler, send or Execute - unless the step itself has
+// work: a random fault process advancing its links, or a late worker whose
+// first request starts at this replica now (client_start).  Otherwise the
+// serial kernel skips such a lane's replica-step
+// whole: no register rows loaded or stored, no counters.  PXS_ROW_DIRTY: the
+// per-replica rows (flags, database version, WPaxos's forwards count) are
+// written back only when they changed.
+#ifndef PXS_SKIP_IDLE
+#define PXS_SKIP_IDLE 1
+#endif
+#ifndef PXS_ROW_DIRTY
+#define PXS_ROW_DIRTY 1
+#endif
+template <int NT>
+__device__ __forceinline__ bool inbox_any(const Rep<NT>& x, uint32_t r, uint32_t b0, uint32_t N) {
+  const uint32_t box0 = (b0 * N + r) * (N + 1u);
+  uint32_t any = 0;
+  for (uint32_t s = 0; s <= N; s++) any |= x.l_cnt[((box0 + s) << 6) | x.lane];
+  return any != 0u;
+}
+template <int NT>
+__device__ __forceinline__ bool late_start(const Params& P, uint32_t t, uint32_t r) {
+  for (uint32_t m = P.late_workers; m; m &= m - 1u) {
+    const uint32_t w = (uint32_t)__builtin_ctz(m);
+    if (P.start_step[w] == t && P.target[w] == r) return true;
+  }
+  return false;
+}
+
 template <int NT, class Proto>
 __device__ __forceinline__ void serial_tile(const Params& P, uint32_t blk, uint32_t bound, uint32_t t0, uint32_t nsteps,
                                             uint4* lds) {
@@ -1450,6 +1515,9 @@ __device__ __forceinline__ void serial_tile(const Params& P, uint32_t blk, uint3
   x.l_cnt = L + (P.img.off_cnt - tail);
   x.l_agn = L + (P.off_agn - tail);
   x.rec = P.rec + (size_t)blk * P.rec_per_block;
+#ifdef PXS_TALLY
+  x.tdbg = P.dbg;
+#endif
   if (P.AR)
     for (uint32_t k = x.lane; k < 2u * N * LANES; k += LANES) x.l_agn[k] = 0;
   if (P.phase_sort)
@@ -1459,6 +1527,7 @@ __device__ __forceinline__ void serial_tile(const Params& P, uint32_t blk, uint3
   x.hw = true;   // every window is in the HBM image here
   x.kc = live ? P.kc[x.c] : 0u;
   uint32_t b0 = t0 % P.D;
+  const bool skip_idle = PXS_SKIP_IDLE && !P.drop_ppm && !P.slow_ppm;
   for (uint32_t t = t0; t < t0 + nsteps; t++) {
     if (PXS_PHASE_RECENT && P.phase_sort && t == t0 + nsteps / 2u)   // the launch's second half only
       for (uint32_t k = 0; k < P.phase_period; k++) reinterpret_cast<uint32_t*>(x.l_cnt + P.ph_rel)[(k << 6) | x.lane] = 0;
@@ -1475,6 +1544,7 @@ __device__ __forceinline__ void serial_tile(const Params& P, uint32_t blk, uint3
 #pragma nounroll
       for (uint32_t k = 0; k < N; k++) {
         const uint32_t r = busy_first<NT, Proto>() ? (uint32_t)(order >> (4u * k)) & 15u : k;
+        if (skip_idle && !inbox_any<NT>(x, r, b0, N) && !late_start<NT>(P, t, r)) continue;
         x.r = r;
         x.t = t;
         x.b0 = b0;
@@ -1484,8 +1554,13 @@ __device__ __forceinline__ void serial_tile(const Params& P, uint32_t blk, uint3
         x.l_b = reinterpret_cast<uint32_t*>(img + P.img.off_b);
         x.l_c = reinterpret_cast<uint32_t*>(img + P.img.off_c);
         const size_t i = rc(P, r, x.c);
+        PXS_TALLY_AT(P, x.blk, TC_ROW_LD, &P.flags[i], false);
         x.flags = P.flags[i];
         x.kvver = P.kv ? P.kv_ver[i] : 0u;
+#ifdef PXS_TALLY
+        if (P.kv) PXS_TALLY_AT(P, x.blk, TC_ROW_LD, &P.kv_ver[i], false);
+#endif
+        const uint32_t flags0 = x.flags, kvver0 = x.kvver;
         Proto::template load<NT>(P, x);
         if constexpr (Proto::step_scratch) Proto::template step_begin<NT>(P, x, L + (P.off_wscr - tail));
         rep_counters_zero<NT>(x);
@@ -1507,8 +1582,14 @@ __device__ __forceinline__ void serial_tile(const Params& P, uint32_t blk, uint3
         replica_step<NT, Proto, false>(P, x);
 #endif
         wb_flush<NT>(x);
-        P.flags[i] = x.flags;
-        if (P.kv) P.kv_ver[i] = x.kvver;
+        if (!PXS_ROW_DIRTY || x.flags != flags0) {
+          PXS_TALLY_AT(P, x.blk, TC_ROW_ST, &P.flags[i], true);
+          P.flags[i] = x.flags;
+        }
+        if (P.kv && (!PXS_ROW_DIRTY || x.kvver != kvver0)) {
+          PXS_TALLY_AT(P, x.blk, TC_ROW_ST, &P.kv_ver[i], true);
+          P.kv_ver[i] = x.kvver;
+        }
         Proto::template store<NT>(P, x);
         if constexpr (Proto::step_scratch) Proto::template step_end<NT>(P, x);
         rep_counters_flush<NT>(P, x);

@@ -55,6 +55,7 @@ __device__ __forceinline__ void wp_bind(const Params& P, Rep<NT>& x, uint32_t ke
     b.y = b.z = 0u;                  // the digest: loaded by exec when it needs it (digest_need)
     x.dig_st = 0u;
   } else {
+    PXS_TALLY_AT(P, x.blk, TC_INST_LD, &P.wst[2 * si], false);
     a = P.wst[2 * si];
     b = P.wst[2 * si + 1];
   }
@@ -94,6 +95,7 @@ __device__ __forceinline__ void wp_unbind(const Params& P, const Rep<NT>& x) {
     w[256] = x.pol | (x.cmask << 16);
     if (x.dig_st == 2u) P.wdig[si] = x.digest;
   } else {
+    PXS_TALLY_AT(P, x.blk, TC_INST_ST, &P.wst[2 * si], true);
     P.wst[2 * si] = make_uint4(x.ballot, (uint32_t)x.slot, (uint32_t)x.execute, meta);
     P.wst[2 * si + 1] = make_uint4(x.npend, (uint32_t)x.digest, (uint32_t)(x.digest >> 32), x.pol | (x.cmask << 16));
   }
@@ -112,6 +114,8 @@ __device__ __forceinline__ bool wp_get(Rep<NT>& x) {
 // majority interval starts now (policy.go:35, NewPolicy)
 template <int NT>
 __device__ __forceinline__ void wp_create(const Params& P, Rep<NT>& x) {
+  if (!x.exists && P.policy == PAXISIM_POLICY_MAJORITY)
+    PXS_TALLY_AT(P, x.blk, TC_OTHER, &P.wpx[3 * wp_slot<NT>(P, x, x.key) + 2], true);
   if (!x.exists && P.policy == PAXISIM_POLICY_MAJORITY)
     P.wpx[3 * wp_slot<NT>(P, x, x.key) + 2] = make_uint4(0u, x.t, 0u, 0u);
   x.exists = 1;
@@ -258,10 +262,12 @@ struct WPaxosProtoT {
   static constexpr uint32_t kind = PAXISIM_WPAXOS;
   template <int NT>
   __device__ static __forceinline__ void load(const Params& P, Rep<NT>& x) {
+    PXS_TALLY_AT(P, x.blk, TC_ROW_LD, &P.nfwd[rc(P, x.r, x.c)], false);
     x.l_inst = x.l_a;                // image region a: the instance scalars (LDS layout)
     x.ikst = (nrep<NT>(P) * WP_WORDS) << 6;
     x.iro = (x.r * WP_WORDS) << 6;
     x.nfwd = P.nfwd[rc(P, x.r, x.c)];
+    x.nfwd0 = x.nfwd;
     x.e0 = 0;                        // entry of slot s: word 4*(s & (W-1)) of the lane's window
     x.es = 4;
     x.pstride = 1;
@@ -283,6 +289,8 @@ struct WPaxosProtoT {
   }
   template <int NT>
   __device__ static __forceinline__ void store(const Params& P, const Rep<NT>& x) {
+    if (PXS_ROW_DIRTY && x.nfwd == x.nfwd0) return;       // unchanged (sim_core.h)
+    PXS_TALLY_AT(P, x.blk, TC_ROW_ST, &P.nfwd[rc(P, x.r, x.c)], true);
     P.nfwd[rc(P, x.r, x.c)] = x.nfwd;
   }
   // The serial kernel (sim_core.h) runs one replica at a time: the instance

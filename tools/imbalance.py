@@ -103,6 +103,43 @@ def main():
     Xp = Ml[h:T].reshape(T - h, L // 64, 64, -1)
     res["busiest_first"] = float((-np.sort(-Xp, axis=3)).max(axis=2).sum() / (Ml[h:T].sum() / 64.0))
     res["lane_total_bound"] = float(Xp.sum(axis=3).max(axis=2).sum() / (Ml[h:T].sum() / 64.0))
+    # Cluster pools (round-5 verdict item 3).  A workgroup of `lanes` lanes
+    # (lanes / 64 waves) owns 256 clusters in the binned order; at each
+    # (step, replica r) the 256 clusters' replica-r inboxes are a pool: a lane
+    # takes the next pending cluster whenever it has drained one (greedy list
+    # scheduling, `switch` trips per cluster taken: its registers and first
+    # record).  The workgroup's waves share the pool, so they meet at a barrier
+    # per (step, replica): a phase holds all of its waves for its slowest
+    # wave's trips.  slot_time = sum over phases of waves x the slowest wave,
+    # over the mean-lane trips (the static kernel: each wave alone, no barrier,
+    # = phase3_binned).  The LDS image is per cluster (about 17.3 KB per 64), so
+    # a 256-cluster workgroup takes 69 KB and a CU holds 2 of them: 2 x waves
+    # per CU, against 8 today.  rate_vs_static = (waves per CU / 8) x
+    # (static cost / slot_time): latency-bound waves each run at their own pace.
+    order = shuf[np.argsort(cls[shuf], kind="stable")]
+    Xb = Ml[h:T][:, order, :]
+    Lg = L // 256 * 256
+    static = res["phase3_binned"]
+
+    def pool_cost(lanes, switch):
+        tot = 0.0
+        for t in range(T - h):
+            for g in range(0, Lg, 256):
+                for r in range(Xb.shape[2]):
+                    free = np.zeros(lanes)
+                    for v in Xb[t, g:g + 256, r]:         # cluster order: the next pending one
+                        k = int(np.argmin(free))
+                        free[k] += v + (switch if v else 0)
+                    tot += (lanes // 64) * free.reshape(lanes // 64, 64).max(axis=1).max()
+        return float(tot / (Xb[:, :Lg].sum() / 64.0))
+
+    res["pool"] = {"metric": "slot_time (see tools/imbalance.py) and rate against the static binned kernel",
+                   "static_binned_cost": static}
+    for lanes in (256, 128, 64):
+        for sw in (0, 1, 2):
+            st_ = pool_cost(lanes, sw)
+            res["pool"][f"{lanes}_lanes_switch{sw}"] = {"slot_time": st_,
+                                                        "rate_vs_static": (2 * lanes / 64) / 8 * static / st_}
     x = lead.astype(float) - lead.mean(axis=0)
     res["leader_autocorrelation"] = {str(g): float((x[g:] * x[:-g]).sum() / (x * x).sum()) for g in range(1, 7)}
     out = json.dumps(res, indent=1)
