@@ -2131,12 +2131,13 @@ extern "C" int paxisim_dist_stats(paxisim_dist* d, paxisim_stats* out, double* k
   return 0;
 }
 
-#if defined(PXS_WAVE_TIMES) && !defined(PXS_STAMPS)
+#if (defined(PXS_WAVE_TIMES) || defined(PXS_TALLY)) && !defined(PXS_STAMPS)
 constexpr uint32_t DBG_PER = 48;   // the stamps build's buffer size (paxisim_dev.h); two words per block used
 #endif
-#if defined(PXS_STAMPS) || defined(PXS_WAVE_TIMES)
+#if defined(PXS_STAMPS) || defined(PXS_WAVE_TIMES) || defined(PXS_TALLY)
 // Diagnostic builds only: per (block, replica) {setup, loop, barrier cycles, loop trips, records, steps}
-// (PXS_STAMPS), or per block the serial kernel's start and end clock (PXS_WAVE_TIMES, tools/wave_times.py).
+// (PXS_STAMPS), per block the serial kernel's start and end clock (PXS_WAVE_TIMES, tools/wave_times.py), or
+// per block the access-class tallies (PXS_TALLY, tools/tally.py).
 extern "C" int paxisim_dbg_enable(paxisim* h) {
   HIPCHK(hipSetDevice(h->cfg.device));
   const size_t n = (h->P.C / LANES) * 16 * DBG_PER;

@@ -133,6 +133,26 @@ def main():
                     tot += (lanes // 64) * free.reshape(lanes // 64, 64).max(axis=1).max()
         return float(tot / (Xb[:, :Lg].sum() / 64.0))
 
+    # The same pool with one barrier per step instead of per (step, replica):
+    # replica-steps of one step are independent, so a wave takes batches of up
+    # to 64 pending non-empty (cluster, r) items of the lowest pending r, its
+    # lanes coherent on r; a batch costs its largest item (+ switch per item
+    # taken, once per batch: the lanes switch together), batches go to the
+    # least-loaded of the 4 waves, and a step holds all 4 for its slowest.
+    def step_pool_cost(switch):
+        tot = 0.0
+        for t in range(T - h):
+            for g in range(0, Lg, 256):
+                load = np.zeros(4)
+                for r in range(Xb.shape[2]):
+                    items = Xb[t, g:g + 256, r]
+                    items = items[items > 0]
+                    for b in range(0, len(items), 64):
+                        k = int(np.argmin(load))
+                        load[k] += items[b:b + 64].max() + switch
+                tot += 4 * load.max()
+        return float(tot / (Xb[:, :Lg].sum() / 64.0))
+
     res["pool"] = {"metric": "slot_time (see tools/imbalance.py) and rate against the static binned kernel",
                    "static_binned_cost": static}
     for lanes in (256, 128, 64):
@@ -140,6 +160,9 @@ def main():
             st_ = pool_cost(lanes, sw)
             res["pool"][f"{lanes}_lanes_switch{sw}"] = {"slot_time": st_,
                                                         "rate_vs_static": (2 * lanes / 64) / 8 * static / st_}
+    for sw in (0, 1, 2):
+        st_ = step_pool_cost(sw)
+        res["pool"][f"step_barrier_256_lanes_switch{sw}"] = {"slot_time": st_, "rate_vs_static": static / st_}
     x = lead.astype(float) - lead.mean(axis=0)
     res["leader_autocorrelation"] = {str(g): float((x[g:] * x[:-g]).sum() / (x * x).sum()) for g in range(1, 7)}
     out = json.dumps(res, indent=1)
