@@ -437,7 +437,7 @@ __global__ void read_log_kernel(Params P, uint64_t cl, uint32_t r, uint32_t key,
     uint4 a, b;
     wp_read(P, blk, key, r, lane, a, b);
     execute = (int32_t)a.z;
-    const uint32_t* e = P.wlog + (si * P.W + w) * 4u;
+    const uint32_t* e = P.wlog + si * P.wlog_str + w * 4u;
     eb = e[0]; ec = e[1]; ea = e[2]; ex = e[3];
   } else {
     execute = (int32_t)P.execute[rc(P, r, c)];
@@ -1067,6 +1067,10 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     const bool ser = serial_for(P.protocol);
     P.wlds = (ev ? atoi(ev) != 0 : !ser) &&
              (ser || proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D, 1).bytes + agn <= LDS_MAX);
+    // PAXISIM_WCOLOC=1: each instance's 32-B scalars and its window in one block of whole lines
+    // (DESIGN.md §5.10); a layout only, the kernels address both through wst_str / wlog_str
+    const char* cv = getenv("PAXISIM_WCOLOC");
+    P.wcoloc = !P.wlds && cv && atoi(cv) != 0;
   }
   P.img = proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D, P.wlds);
   {
@@ -1146,9 +1150,19 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     uint4* gst = carve<uint4>(p, NIC * GMAX);
     uint32_t* st = carve<uint32_t>(p, NC * NSTAT);
     uint32_t* reqx = carve<uint32_t>(p, wp ? 0 : NC * P.W);
-    uint4* wst = carve<uint4>(p, wp && !P.wlds ? NIC * 2 : 0);
+    // WPaxos instances: the scalars table and the windows apart, or (wcoloc) one block per instance
+    // holding both - 32 B of scalars, then the window - padded to whole 128-B lines, so the entries
+    // at the window's head share the line the bind loads
+    const bool coloc = wp && !P.wlds && P.wcoloc;
+    const size_t wblk_b = ((32u + 16u * P.W) + 127u) & ~size_t(127);
+    uint4* wblk = carve<uint4>(p, coloc ? NIC * (wblk_b / 16u) : 0);
+    uint4* wst = carve<uint4>(p, wp && !P.wlds && !coloc ? NIC * 2 : 0);
     uint64_t* wdig = carve<uint64_t>(p, wp && P.wlds ? NIC : 0);
-    uint32_t* wlog = carve<uint32_t>(p, wp ? NIC * P.W * 4 : 0);
+    uint32_t* wlog = carve<uint32_t>(p, wp && !coloc ? NIC * P.W * 4 : 0);
+    if (coloc) {
+      wst = wblk;
+      wlog = reinterpret_cast<uint32_t*>(wblk) + 8;
+    }
     uint32_t* wpend = carve<uint32_t>(p, wp ? NIC * PMAX : 0);
     uint4* wpx = carve<uint4>(p, wp && cfg->policy != PAXISIM_POLICY_CONSECUTIVE ? NIC * 3 : 0);
     uint4* hist = carve<uint4>(p, NC * P.H);
@@ -1174,6 +1188,8 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
       P.link_drop = links; P.link_slow = links + NC * N;
       P.ck_e = cke; P.ck_d = ckd; P.stats = st; P.reqx = reqx; P.hist = hist; P.image = image; P.rec = rec;
       P.wst = wst; P.wdig = wdig; P.wlog = wlog; P.wpend = wpend; P.gst = gst; P.wpx = wpx;
+      P.wst_str = coloc ? (uint32_t)(wblk_b / 16u) : 2u;
+      P.wlog_str = coloc ? (uint32_t)(wblk_b / 4u) : P.W * 4u;
       P.slot_of = maps; P.cl_of = maps + C; P.frz = maps + 2 * C; P.qf = maps + 3 * C;
       P.phase = phs;
       P.agr = agr;

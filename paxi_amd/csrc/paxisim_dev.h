@@ -142,10 +142,13 @@ struct Params {
   // WPaxos kpaxos instances, one 32-B state + a W-entry window + PMAX pending per
   // (blk, key, r, lane): {ballot, slot, execute, active|exists<<1|p1acks<<16,
   // npend, digest lo, digest hi, policy last|hits<<8}; entries {ballot, cmd|flags, acks, request}
-  uint4* wst;            // [blk][K][N][64][2] (wlds = 0)
+  uint4* wst;            // [blk][K][N][64] x wst_str uint4 (wlds = 0): {ballot..meta}, {npend, digest, pol|cmask}
+  uint32_t wst_str;      // uint4s between instances: 2, or (wcoloc) the co-located block's size / 16
+  uint32_t wlog_str;     // u32s between instances' windows: W * 4, or (wcoloc) the block's size / 4
   uint32_t wlds;         // 1: instance scalars in the tile image (region a, LDS during a launch), digests in wdig
+  uint32_t wcoloc;       // 1 (wlds = 0): an instance's scalars and window in one block (PAXISIM_WCOLOC)
   uint64_t* wdig;        // [blk][K][N][64] instance digests (wlds = 1)
-  uint32_t* wlog;        // [blk][K][N][64][W][4]
+  uint32_t* wlog;        // [blk][K][N][64][W][4]; wcoloc: 32 B into each instance's block, after its wst
   uint32_t* wpend;       // [blk][K][N][64][PMAX]
   uint4* wpx;            // [blk][K][N][64][3] majority {hits u16 x 16 (2 x uint4), {sum, start step}} / ema {s lo, s hi, zone}
   uint32_t* stats;       // [NSTAT][N][C]
@@ -223,8 +226,8 @@ __device__ __forceinline__ void wp_read(const Params& P, uint64_t blk, uint32_t 
                                         uint4& b) {
   const size_t si = wp_si(P, blk, k, r, lane);
   if (!P.wlds) {
-    a = P.wst[2 * si];
-    b = P.wst[2 * si + 1];
+    a = P.wst[(size_t)P.wst_str * si];
+    b = P.wst[(size_t)P.wst_str * si + 1];
     return;
   }
   const uint32_t* w = wp_img(P, blk, k, r, lane);
@@ -236,8 +239,8 @@ __device__ __forceinline__ void wp_write(const Params& P, uint64_t blk, uint32_t
                                          const uint4& a, const uint4& b) {
   const size_t si = wp_si(P, blk, k, r, lane);
   if (!P.wlds) {
-    P.wst[2 * si] = a;
-    P.wst[2 * si + 1] = b;
+    P.wst[(size_t)P.wst_str * si] = a;
+    P.wst[(size_t)P.wst_str * si + 1] = b;
     return;
   }
   uint32_t* w = wp_img(P, blk, k, r, lane);

@@ -55,9 +55,9 @@ __device__ __forceinline__ void wp_bind(const Params& P, Rep<NT>& x, uint32_t ke
     b.y = b.z = 0u;                  // the digest: loaded by exec when it needs it (digest_need)
     x.dig_st = 0u;
   } else {
-    PXS_TALLY_AT(P, x.blk, TC_INST_LD, &P.wst[2 * si], false);
-    a = P.wst[2 * si];
-    b = P.wst[2 * si + 1];
+    PXS_TALLY_AT(P, x.blk, TC_INST_LD, &P.wst[(size_t)P.wst_str * si], false);
+    a = P.wst[(size_t)P.wst_str * si];
+    b = P.wst[(size_t)P.wst_str * si + 1];
   }
   x.key = key;
   x.ktag = key << 16;
@@ -74,7 +74,7 @@ __device__ __forceinline__ void wp_bind(const Params& P, Rep<NT>& x, uint32_t ke
   if constexpr (!LDS) x.dig_st = 1u;
   x.pol = b.w & 0xFFFFu;
   x.cmask = b.w >> 16;
-  uint32_t* lb = P.wlog + si * P.W * 4u;
+  uint32_t* lb = P.wlog + si * P.wlog_str;
   x.l_a = lb;
   x.l_b = lb + 1;
   x.l_c = lb + 2;
@@ -95,9 +95,9 @@ __device__ __forceinline__ void wp_unbind(const Params& P, const Rep<NT>& x) {
     w[256] = x.pol | (x.cmask << 16);
     if (x.dig_st == 2u) P.wdig[si] = x.digest;
   } else {
-    PXS_TALLY_AT(P, x.blk, TC_INST_ST, &P.wst[2 * si], true);
-    P.wst[2 * si] = make_uint4(x.ballot, (uint32_t)x.slot, (uint32_t)x.execute, meta);
-    P.wst[2 * si + 1] = make_uint4(x.npend, (uint32_t)x.digest, (uint32_t)(x.digest >> 32), x.pol | (x.cmask << 16));
+    PXS_TALLY_AT(P, x.blk, TC_INST_ST, &P.wst[(size_t)P.wst_str * si], true);
+    P.wst[(size_t)P.wst_str * si] = make_uint4(x.ballot, (uint32_t)x.slot, (uint32_t)x.execute, meta);
+    P.wst[(size_t)P.wst_str * si + 1] = make_uint4(x.npend, (uint32_t)x.digest, (uint32_t)(x.digest >> 32), x.pol | (x.cmask << 16));
   }
 }
 

@@ -117,14 +117,16 @@ def test_majority_and_ema_policies(policy, kw):
     assert st["delivered"]["LeaderChange"] > 0
 
 
-@pytest.mark.parametrize("wlds", ["0", "1"])
-def test_both_instance_layouts(wlds, monkeypatch):
-    """The serial kernel's two homes for the kpaxos scalars - the packed HBM
-    table (default since round 4) and the tile image's word planes
-    (PAXISIM_WLDS=1) - under faults, with the Database on: both equal the
-    oracle.  (Round 3's first serial WPaxos build lost instance state between
-    replica-steps; this keeps both layouts under test.)"""
+@pytest.mark.parametrize("wlds,wcoloc", [("0", "0"), ("1", "0"), ("0", "1")])
+def test_both_instance_layouts(wlds, wcoloc, monkeypatch):
+    """The serial kernel's homes for the kpaxos scalars - the packed HBM
+    table (default since round 4), the tile image's word planes
+    (PAXISIM_WLDS=1) and (round 6, PAXISIM_WCOLOC=1) one block per instance
+    holding its scalars and its window - under faults, with the Database on:
+    all equal the oracle.  (Round 3's first serial WPaxos build lost instance
+    state between replica-steps; this keeps every layout under test.)"""
     monkeypatch.setenv("PAXISIM_WLDS", wlds)
+    monkeypatch.setenv("PAXISIM_WCOLOC", wcoloc)
     wl = abi.make_workload(outstanding=9, target=list(range(9)), locality_ppm=700_000, write_ppm=600_000)
     fp = abi.make_fault_process(drop_ppm=1000, drop_len=10, slow_ppm=2000, slow_len=10, slow_min=1, slow_max=2)
     st = run_and_compare(wp_config(130, max_delay=2, kv=1), wl, fp, chunks=(120, 97))

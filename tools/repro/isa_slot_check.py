@@ -63,7 +63,7 @@ def writes(instr, reg):
 def main():
     path, csrc = sys.argv[1], sys.argv[2]
     ins = parse(path)
-    unbind = src_line(csrc, "wpaxos_kernel.h", "P.wst[2 * si] = make_uint4(x.ballot")
+    unbind = src_line(csrc, "wpaxos_kernel.h", "] = make_uint4(x.ballot, (uint32_t)x.slot")
     p1b_send = src_line(csrc, "paxos_kernel.h", "send_begin<NT>(P, x, bal_id(mb)")
     stores = [(n, s) for n, s, ch in ins
               if s.startswith("global_store_dwordx4") and re.match(rf"(\S*/)?wpaxos_kernel\.h:{unbind}:", ch)]
