@@ -1067,10 +1067,12 @@ extern "C" int paxisim_create(const paxisim_config* cfg, const paxisim_workload*
     const bool ser = serial_for(P.protocol);
     P.wlds = (ev ? atoi(ev) != 0 : !ser) &&
              (ser || proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D, 1).bytes + agn <= LDS_MAX);
-    // PAXISIM_WCOLOC=1: each instance's 32-B scalars and its window in one block of whole lines
-    // (DESIGN.md §5.10); a layout only, the kernels address both through wst_str / wlog_str
+    // Each instance's 32-B scalars and its window in one block of whole lines: a
+    // layout only, the kernels address both through wst_str / wlog_str.  On by default at W = 8, where
+    // six of the eight entries share the line the bind loads (mirrored A/B r6g2, config 5: +4.2% over
+    // the packed table at W = 8); at W = 16 it is 6% slower (r6g1).  PAXISIM_WCOLOC=0/1 overrides.
     const char* cv = getenv("PAXISIM_WCOLOC");
-    P.wcoloc = !P.wlds && cv && atoi(cv) != 0;
+    P.wcoloc = !P.wlds && (cv ? atoi(cv) != 0 : P.W == 8u);
   }
   P.img = proto_image(P.protocol, N, P.W, P.keys, P.WK, P.D, P.wlds);
   {

@@ -24,7 +24,6 @@ struct Rep {
   uint32_t ballot;
   int32_t slot, execute;
   uint32_t active, p1mask, flags, npend, nfwd;
-  uint32_t nfwd0;                       // WPaxos: nfwd as loaded (the row is written back only if it changed)
   uint64_t digest;
   // the bound Paxos instance (Multi-Paxos: the replica's one; WPaxos: one kpaxos per key)
   uint32_t inst;                        // instance index in [NI] tables (key * N + r)
@@ -1456,16 +1455,21 @@ template <class Proto> constexpr int serial_waves() {
 // message there is no handler, send or Execute - unless the step itself has
 // work: a random fault process advancing its links, or a late worker whose
 // first request starts at this replica now (client_start).  Otherwise the
-// serial kernel skips such a lane's replica-step
-// whole: no register rows loaded or stored, no counters.  PXS_ROW_DIRTY: the
-// per-replica rows (flags, database version, WPaxos's forwards count) are
-// written back only when they changed.
+// serial kernel skips such a lane's replica-step whole: no register rows
+// loaded or stored, no counters.  PXS_ROW_DIRTY: the per-replica rows (flags,
+// database version) are written back only when they changed.  Both are on for
+// ABD only: mirrored A/Bs (gpurun_out/r6g2) give ABD (config 3) +4.4%, but
+// Multi-Paxos (config 2, where the random fault process leaves no replica-step
+// idle) -2% and WPaxos (config 5: 0.4% of replica-steps idle) -8%; the saved
+// values and the inbox test cost those kernels registers.
 #ifndef PXS_SKIP_IDLE
 #define PXS_SKIP_IDLE 1
 #endif
 #ifndef PXS_ROW_DIRTY
 #define PXS_ROW_DIRTY 1
 #endif
+template <class Proto> constexpr bool skip_idle_on() { return PXS_SKIP_IDLE && Proto::kind == PAXISIM_ABD; }
+template <class Proto> constexpr bool row_dirty_on() { return PXS_ROW_DIRTY && Proto::kind == PAXISIM_ABD; }
 template <int NT>
 __device__ __forceinline__ bool inbox_any(const Rep<NT>& x, uint32_t r, uint32_t b0, uint32_t N) {
   const uint32_t box0 = (b0 * N + r) * (N + 1u);
@@ -1527,7 +1531,7 @@ __device__ __forceinline__ void serial_tile(const Params& P, uint32_t blk, uint3
   x.hw = true;   // every window is in the HBM image here
   x.kc = live ? P.kc[x.c] : 0u;
   uint32_t b0 = t0 % P.D;
-  const bool skip_idle = PXS_SKIP_IDLE && !P.drop_ppm && !P.slow_ppm;
+  const bool skip_idle = skip_idle_on<Proto>() && !P.drop_ppm && !P.slow_ppm;
   for (uint32_t t = t0; t < t0 + nsteps; t++) {
     if (PXS_PHASE_RECENT && P.phase_sort && t == t0 + nsteps / 2u)   // the launch's second half only
       for (uint32_t k = 0; k < P.phase_period; k++) reinterpret_cast<uint32_t*>(x.l_cnt + P.ph_rel)[(k << 6) | x.lane] = 0;
@@ -1544,7 +1548,8 @@ __device__ __forceinline__ void serial_tile(const Params& P, uint32_t blk, uint3
 #pragma nounroll
       for (uint32_t k = 0; k < N; k++) {
         const uint32_t r = busy_first<NT, Proto>() ? (uint32_t)(order >> (4u * k)) & 15u : k;
-        if (skip_idle && !inbox_any<NT>(x, r, b0, N) && !late_start<NT>(P, t, r)) continue;
+        if constexpr (skip_idle_on<Proto>())
+          if (skip_idle && !inbox_any<NT>(x, r, b0, N) && !late_start<NT>(P, t, r)) continue;
         x.r = r;
         x.t = t;
         x.b0 = b0;
@@ -1560,7 +1565,7 @@ __device__ __forceinline__ void serial_tile(const Params& P, uint32_t blk, uint3
 #ifdef PXS_TALLY
         if (P.kv) PXS_TALLY_AT(P, x.blk, TC_ROW_LD, &P.kv_ver[i], false);
 #endif
-        const uint32_t flags0 = x.flags, kvver0 = x.kvver;
+        const uint32_t flags0 = row_dirty_on<Proto>() ? x.flags : 0u, kvver0 = row_dirty_on<Proto>() ? x.kvver : 0u;
         Proto::template load<NT>(P, x);
         if constexpr (Proto::step_scratch) Proto::template step_begin<NT>(P, x, L + (P.off_wscr - tail));
         rep_counters_zero<NT>(x);
@@ -1582,11 +1587,11 @@ __device__ __forceinline__ void serial_tile(const Params& P, uint32_t blk, uint3
         replica_step<NT, Proto, false>(P, x);
 #endif
         wb_flush<NT>(x);
-        if (!PXS_ROW_DIRTY || x.flags != flags0) {
+        if (!row_dirty_on<Proto>() || x.flags != flags0) {
           PXS_TALLY_AT(P, x.blk, TC_ROW_ST, &P.flags[i], true);
           P.flags[i] = x.flags;
         }
-        if (P.kv && (!PXS_ROW_DIRTY || x.kvver != kvver0)) {
+        if (P.kv && (!row_dirty_on<Proto>() || x.kvver != kvver0)) {
           PXS_TALLY_AT(P, x.blk, TC_ROW_ST, &P.kv_ver[i], true);
           P.kv_ver[i] = x.kvver;
         }

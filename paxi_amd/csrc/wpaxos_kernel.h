@@ -267,7 +267,6 @@ struct WPaxosProtoT {
     x.ikst = (nrep<NT>(P) * WP_WORDS) << 6;
     x.iro = (x.r * WP_WORDS) << 6;
     x.nfwd = P.nfwd[rc(P, x.r, x.c)];
-    x.nfwd0 = x.nfwd;
     x.e0 = 0;                        // entry of slot s: word 4*(s & (W-1)) of the lane's window
     x.es = 4;
     x.pstride = 1;
@@ -289,7 +288,6 @@ struct WPaxosProtoT {
   }
   template <int NT>
   __device__ static __forceinline__ void store(const Params& P, const Rep<NT>& x) {
-    if (PXS_ROW_DIRTY && x.nfwd == x.nfwd0) return;       // unchanged (sim_core.h)
     PXS_TALLY_AT(P, x.blk, TC_ROW_ST, &P.nfwd[rc(P, x.r, x.c)], true);
     P.nfwd[rc(P, x.r, x.c)] = x.nfwd;
   }

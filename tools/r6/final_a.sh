@@ -14,3 +14,7 @@ step traffic3 300 bash tools/traffic.sh 3
 step traffic4 300 bash tools/traffic.sh 4
 step traffic4_fz0 300 bash tools/traffic.sh 4 --fz 0
 step traffic5 400 bash tools/traffic.sh 5
+# confirmation A/Bs against the round-5 code path (var/v_base.so: no idle skip, no dirty rows, packed
+# WPaxos table): config 2 must be unchanged; config 5 at the new default (window 8, co-located blocks)
+REPS=2 step ab_c2_final 400 tools/ab_env.sh r6fa/ab_c2 "prod|X=1" "r5path|PAXISIM_LIB=var/v_base.so" -- --config 2 --no-shard-check
+REPS=2 step ab_c5_final 500 tools/ab_env.sh r6fa/ab_c5 "prod|X=1" "r5path|PAXISIM_LIB=var/v_base.so BENCH_ARGS=--window 16" -- --config 5 --no-shard-check
