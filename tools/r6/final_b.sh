@@ -14,3 +14,5 @@ P1="SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_
 P3="TCC_HIT_sum TCC_MISS_sum"
 step pmc_c2 400 bash tools/pmc2.sh r6fb_c2 "$P1" "$P3" -- --config 2 --warmup 5 --steps 1
 step pmc_c5 400 bash tools/pmc2.sh r6fb_c5 "$P1" "$P3" -- --config 5 --warmup 5 --steps 1
+# the persistent pipelined form (var/v_persist.so, PXS_PIPE_PERSIST=1, the 5-replica Multi-Paxos unit) against the product
+REPS=2 step abp_c2 400 tools/ab_env.sh r6fb/abp_c2 "prod|X=1" "persist|PAXISIM_LIB=var/v_persist.so" -- --config 2 --no-shard-check
