@@ -42,7 +42,7 @@ def test_traffic_record_attaches_only_to_its_own_run(name):
 
 @pytest.mark.parametrize("name", CONFIGS)
 def test_final_bench_lines_carry_their_builds_traffic(name):
-    line = json.loads(open(os.path.join(ROOT, "profiles", "r5final", f"bench_config{name}.json")).read())
+    line = json.loads(open(os.path.join(ROOT, "profiles", "r6final", f"bench_config{name}.json")).read())
     r, t = line["roofline"], _record(name)
     assert line["build_id"] == t["build_id"] and line["build_matches_sources"]
     assert r["traffic"] == pytest.approx(t["bytes_per_launch"]) and r["kernel"] == t["kernel"]
