@@ -1461,15 +1461,29 @@ template <class Proto> constexpr int serial_waves() {
 // ABD only: mirrored A/Bs (gpurun_out/r6g2) give ABD (config 3) +4.4%, but
 // Multi-Paxos (config 2, where the random fault process leaves no replica-step
 // idle) -2% and WPaxos (config 5: 0.4% of replica-steps idle) -8%; the saved
-// values and the inbox test cost those kernels registers.
+// values and the inbox test cost those kernels registers.  The skip alone is
+// on in the 9-replica Multi-Paxos unit (PXS_SKIP_IDLE_PAXOS, __graft_entry__
+// TU_FLAGS): config 4 has no random fault process and 41% of its wave-level
+// replica-steps are idle (phase-aligned followers), +6.3% (gpurun_out/r6o;
+// with the dirty rows too only +2.6%).
 #ifndef PXS_SKIP_IDLE
 #define PXS_SKIP_IDLE 1
 #endif
 #ifndef PXS_ROW_DIRTY
 #define PXS_ROW_DIRTY 1
 #endif
-template <class Proto> constexpr bool skip_idle_on() { return PXS_SKIP_IDLE && Proto::kind == PAXISIM_ABD; }
-template <class Proto> constexpr bool row_dirty_on() { return PXS_ROW_DIRTY && Proto::kind == PAXISIM_ABD; }
+#ifndef PXS_SKIP_IDLE_PAXOS
+#define PXS_SKIP_IDLE_PAXOS 0
+#endif
+#ifndef PXS_ROW_DIRTY_PAXOS
+#define PXS_ROW_DIRTY_PAXOS 0
+#endif
+template <class Proto> constexpr bool skip_idle_on() {
+  return PXS_SKIP_IDLE && (Proto::kind == PAXISIM_ABD || (PXS_SKIP_IDLE_PAXOS && Proto::kind == PAXISIM_PAXOS));
+}
+template <class Proto> constexpr bool row_dirty_on() {
+  return PXS_ROW_DIRTY && (Proto::kind == PAXISIM_ABD || (PXS_ROW_DIRTY_PAXOS && Proto::kind == PAXISIM_PAXOS));
+}
 template <int NT>
 __device__ __forceinline__ bool inbox_any(const Rep<NT>& x, uint32_t r, uint32_t b0, uint32_t N) {
   const uint32_t box0 = (b0 * N + r) * (N + 1u);
