@@ -4,7 +4,7 @@
 # records go into profiles/ before call 2's bench lines, which attach them by build id.
 set -o pipefail
 cd "$(dirname "$0")/../.."
-O=gpurun_out/r6fa2; mkdir -p $O
+O=gpurun_out/r6fa3; mkdir -p $O
 . tools/r6/step.sh
 export TMPDIR=/tmp
 step pytest 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu
@@ -14,7 +14,5 @@ step traffic3 300 bash tools/traffic.sh 3
 step traffic4 300 bash tools/traffic.sh 4
 step traffic4_fz0 300 bash tools/traffic.sh 4 --fz 0
 step traffic5 400 bash tools/traffic.sh 5
-# confirmation A/Bs against the round-5 code path (var/v_base.so: no idle skip, no dirty rows, packed
-# WPaxos table): config 2 must be unchanged; config 5 at the new default (window 8, co-located blocks)
-REPS=2 step ab_c2_final 400 tools/ab_env.sh r6fa2/ab_c2 "prod|X=1" "r5path|PAXISIM_LIB=var/v_base.so" -- --config 2 --no-shard-check
-REPS=2 step ab_c5_final 500 tools/ab_env.sh r6fa2/ab_c5 "prod|X=1" "r5path|PAXISIM_LIB=var/v_base.so BENCH_ARGS=--window 16" -- --config 5 --no-shard-check
+# ABD with idle-skip but without the dirty rows (var/v_abdnodirty.so), mirrored, for the record
+REPS=2 step abd_c3 500 tools/ab_env.sh r6fa3/abd_c3 "prod|X=1" "nodirty|PAXISIM_LIB=var/v_abdnodirty.so" -- --config 3 --no-shard-check
